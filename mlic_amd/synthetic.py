@@ -1,0 +1,170 @@
+"""Seeded synthetic weights and images (no checkpoints or datasets exist offline).
+
+Weights: every state_dict key of `spec.state_dict_shapes(name)` is drawn from a
+numpy PCG64 stream keyed by (seed, crc32(key)), so the values are independent of
+key order and identical on every machine.  Plain default init is degenerate for
+this model (std(y) = 0.14 and 100 % of y rounds to 0), so the set is
+*conditioned*: fan-in-scaled gaussians, then a few fixed multipliers/offsets
+(`_CONDITION`) chosen so that y has std of a few units, predicted scales spread
+over the scale table, z is non-trivial and x_hat lands around [0, 1].
+
+Images: SURVEY §8(d) "synthetic inputs" — a sum of random-phase 2-D sinusoids +
+gradient + noise, clamped to [0,1] and quantized to k/255.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from typing import Dict
+
+import numpy as np
+import torch
+
+from . import spec
+
+# key-suffix -> (multiplier, additive offset), applied after the base draw.
+# Matched with str.endswith on the key, first match wins; {C} is slice_ch.
+_CONDITION = (
+    # g_a output y: std of a few units so rounding is non-trivial
+    ("g_a.analysis_transform.6.point_conv.weight", 24.0, 0.0),
+    ("g_a.analysis_transform.6.weight", 24.0, 0.0),
+    # h_a output z
+    ("h_a.reduction.8.point_conv.weight", 40.0, 0.0),
+    ("h_a.reduction.8.weight", 40.0, 0.0),
+    # g_s output ~ 0.5 +- small
+    ("g_s.synthesis_transform.7.0.weight", 0.2, 0.0),
+    ("g_s.synthesis_transform.7.0.bias", 0.0, 0.5),
+)
+
+
+_GAIN = 0.7
+
+
+def _rng(seed: int, key: str) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64([int(seed) & 0xFFFFFFFF, zlib.crc32(key.encode())]))
+
+
+def _fan_in(shape) -> int:
+    f = 1
+    for d in shape[1:]:
+        f *= d
+    return max(f, 1)
+
+
+def _draw(key: str, shape, cfg: spec.ModelConfig, seed: int) -> np.ndarray:
+    r = _rng(seed, key)
+    leaf = key.rsplit(".", 1)[-1]
+    n = int(np.prod(shape)) if len(shape) else 1
+    # ---- fixed buffers (exact compressai constants) -------------------------
+    if leaf == "pedestal":
+        return np.array([(2.0 ** -18) ** 2], np.float32)
+    if key.endswith("beta_reparam.lower_bound.bound"):
+        return np.array([(1e-6 + (2.0 ** -18) ** 2) ** 0.5], np.float32)
+    if key.endswith("gamma_reparam.lower_bound.bound"):
+        return np.array([(0.0 + (2.0 ** -18) ** 2) ** 0.5], np.float32)
+    if key.endswith("likelihood_lower_bound.bound"):
+        return np.array([1e-9], np.float32)
+    if key.endswith("lower_bound_scale.bound") or key.endswith("scale_bound"):
+        return np.array([0.11], np.float32)
+    if leaf == "target":
+        t = math.log(2 / 1e-9 - 1)
+        return np.array([-t, 0.0, t], np.float32)
+    if leaf == "relative_position_index":
+        return relative_position_index(cfg.context_window)
+    if leaf in spec.DYNAMIC_BUFFERS:
+        return np.zeros(shape, np.int32 if leaf != "scale_table" else np.float32)
+    # ---- entropy bottleneck (compressai init, perturbed) ---------------------
+    if key.startswith("entropy_bottleneck."):
+        f = (1, 3, 3, 3, 3, 1)
+        sc = 10.0 ** (1 / 5)
+        if leaf.startswith("_matrix"):
+            i = int(leaf[-1])
+            base = math.log(math.expm1(1 / sc / f[i + 1]))
+            return (base + 0.3 * r.standard_normal(n)).reshape(shape).astype(np.float32)
+        if leaf.startswith("_bias"):
+            return r.uniform(-0.5, 0.5, n).reshape(shape).astype(np.float32)
+        if leaf.startswith("_factor"):
+            return (0.3 * r.standard_normal(n)).reshape(shape).astype(np.float32)
+        if leaf == "quantiles":
+            med = 0.4 * r.standard_normal(shape[0])
+            q = np.stack([med - 6.0 - r.uniform(0, 4, shape[0]), med, med + 6.0 + r.uniform(0, 4, shape[0])], -1)
+            return q.reshape(shape).astype(np.float32)
+    # ---- GDN (stored in reparametrized form: eff = max(p, bound)^2 - pedestal) --
+    if leaf == "beta":
+        eff = r.uniform(0.8, 1.2, n)
+        return np.sqrt(eff + (2.0 ** -36)).astype(np.float32)
+    if leaf == "gamma":
+        c = shape[0]
+        eff = 0.1 * np.eye(c) + r.uniform(0.0, 0.2 / c, (c, c))
+        return np.sqrt(eff + (2.0 ** -36)).astype(np.float32)
+    # ---- norms / tables --------------------------------------------------------
+    if ".norm" in key and leaf == "weight":
+        return (1.0 + 0.1 * r.standard_normal(n)).reshape(shape).astype(np.float32)
+    if ".norm" in key and leaf == "bias":
+        return (0.1 * r.standard_normal(n)).reshape(shape).astype(np.float32)
+    if leaf == "relative_position_table":
+        return (0.3 * r.standard_normal(n)).reshape(shape).astype(np.float32)
+    if leaf == "Gain":
+        return np.array(spec.VBR_GAIN, np.float32)
+    # ---- conv / linear weights and biases -----------------------------------
+    if leaf == "bias":
+        return (0.05 * r.standard_normal(n)).reshape(shape).astype(np.float32)
+    if leaf == "weight":
+        fan = _fan_in(shape)
+        return (r.standard_normal(n) * (_GAIN / math.sqrt(fan))).reshape(shape).astype(np.float32)
+    raise KeyError(f"no synthesis rule for {key} {shape}")
+
+
+def relative_position_index(window: int) -> np.ndarray:
+    """Swin relative-position index (attention.py:28-39): idx[i, j] =
+    (hi - hj + w - 1) * (2w - 1) + (wi - wj + w - 1) for window cells i, j."""
+    ij = np.arange(window * window)
+    hi, wi = ij // window, ij % window
+    dh = hi[:, None] - hi[None, :] + window - 1
+    dw = wi[:, None] - wi[None, :] + window - 1
+    return (dh * (2 * window - 1) + dw).astype(np.int64)
+
+
+def synth_state_dict(name: str, seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Conditioned synthetic state_dict for model `name` (CPU tensors)."""
+    cfg = spec.get_config(name)
+    out: Dict[str, torch.Tensor] = {}
+    for key, shape in spec.state_dict_shapes(name).items():
+        a = _draw(key, shape, cfg, seed)
+        for suffix, mul, add in _CONDITION:
+            if key.endswith(suffix):
+                a = (a * mul + add).astype(a.dtype)
+                break
+        # entropy-parameter output layer: the first slice_ch outputs are scales
+        # (mlicpp.py:112 chunk order): bias them positive so scales spread over the table
+        if key.endswith(".fusion.6.bias") and key.startswith("entropy_parameters"):
+            a = a.copy()
+            a[: cfg.slice_ch] += 1.2
+        if key.endswith(".fusion.6.weight") and key.startswith("entropy_parameters"):
+            a = a.copy()
+            a[: cfg.slice_ch] *= 40.0
+        out[key] = torch.from_numpy(np.ascontiguousarray(a))
+    return out
+
+
+def synth_image(H: int, W: int, seed: int, kind: str = "smooth") -> torch.Tensor:
+    """One [1, 3, H, W] float32 image in [0, 1] quantized to k/255."""
+    r = np.random.Generator(np.random.PCG64(1234 + int(seed)))
+    if kind == "uniform":
+        img = r.uniform(0, 1, (3, H, W))
+    else:
+        yy, xx = np.meshgrid(np.arange(H, dtype=np.float64), np.arange(W, dtype=np.float64), indexing="ij")
+        img = np.zeros((3, H, W))
+        for c in range(3):
+            acc = 0.5 + 0.15 * (xx / W - 0.5) + 0.1 * (yy / H - 0.5)
+            for _ in range(8):
+                period = r.uniform(8, 512)
+                theta = r.uniform(0, 2 * math.pi)
+                phase = r.uniform(0, 2 * math.pi)
+                amp = r.uniform(0.02, 0.12)
+                acc = acc + amp * np.sin(2 * math.pi * (xx * math.cos(theta) + yy * math.sin(theta)) / period + phase)
+            img[c] = acc
+        img = img + 0.02 * r.standard_normal(img.shape)
+    img = np.clip(img, 0.0, 1.0)
+    img = np.round(img * 255.0) / 255.0
+    return torch.from_numpy(img.astype(np.float32))[None]
