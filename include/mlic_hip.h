@@ -1,0 +1,82 @@
+/* mlic_hip — MI355X-native (gfx950) MLIC++ encode/decode: C ABI.
+ *
+ * Drop-in boundary for the reference's CompressionModel API (MLIC++/models/mlicpp.py):
+ *   mlic_create / mlic_destroy ........ MLICPlusPlus.__init__ + load_state_dict (mlicpp.py:14-77, 461-468);
+ *                                       weights are the reference state_dict tensors, by name
+ *   mlic_forward ...................... MLICPlusPlus.forward (mlicpp.py:79-185); VBR: mlicpp_vbr.py:137-519
+ *   mlic_set_entropy_tables ........... GaussianConditional/EntropyBottleneck CDF buffers after update()
+ *                                       (mlicpp.py:470-475; compressai _quantized_cdf/_cdf_length/_offset)
+ *   mlic_compress / mlic_encoded_* .... MLICPlusPlus.compress (mlicpp.py:199-290) incl. the rANS coder
+ *   mlic_decompress ................... MLICPlusPlus.decompress (mlicpp.py:292-378)
+ *   mlic_pmf_to_quantized_cdf ......... compressai._CXX.pmf_to_quantized_cdf (used by update())
+ *   mlic_rans_encode / mlic_rans_decode  compressai.ans.RansEncoder.encode_with_indexes /
+ *                                       RansDecoder.decode_with_indexes (byte-compatible)
+ *
+ * Conventions: every function returns 0 on success, nonzero on error (message via mlic_last_error(),
+ * thread-local); no C++ exception crosses the ABI.  Tensors are caller-owned device buffers, NCHW
+ * fp32, contiguous.  `stream` is a hipStream_t (NULL = default stream); calls on one handle are
+ * serialised on that stream.  The library owns its packed weights and a per-handle workspace.
+ */
+#ifndef MLIC_HIP_H
+#define MLIC_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mlic_model mlic_model;
+
+const char* mlic_last_error(void);
+const char* mlic_version(void);
+
+/* names/ptrs: n float32 device tensors (state_dict entries, plus "__scale_table" [64]);
+ * shapes: n*4 int64 (unused dims 1), ndims: n */
+int mlic_create(const char* model_name, int n, const char* const* names, const float* const* ptrs,
+                const int64_t* shapes, const int* ndims, void* stream, mlic_model** out);
+int mlic_destroy(mlic_model* m);
+
+/* x [B,3,H,W] (H, W multiples of 64) -> x_hat [B,3,H,W], y_lik [B,M,H/16,W/16], z_lik [B,N,H/64,W/64];
+ * outputs may be NULL.  vbr_scale = Gain[s] for *_VBR models (ignored otherwise, pass 1). */
+int mlic_forward(mlic_model* m, void* stream, const float* x, int B, int H, int W, float* x_hat, float* y_lik,
+                 float* z_lik, float vbr_scale);
+
+int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t* gc_len, const int32_t* gc_off,
+                            int gc_n, int gc_stride, const int32_t* eb_cdf, const int32_t* eb_len,
+                            const int32_t* eb_off, int eb_n, int eb_stride);
+
+int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale);
+int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len);
+int mlic_encoded_copy(mlic_model* m, int b, uint8_t* y, uint8_t* z);
+/* the coder inputs of image b from the last compress(): y symbols/indexes (all phases, coder order)
+ * and z symbols; pass NULL buffers to query the counts */
+int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32_t* y_sym, int32_t* y_idx,
+                         int32_t* z_sym);
+/* y[b], z[b]: host byte strings of image b; hz, wz = latent z grid (shape returned by compress) */
+int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
+                    const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
+                    float vbr_scale);
+
+/* module-level entry points (tests / profiling): which = local|chan|inter|intra|epa|epn|lrpn|g_a|h_a|h_s|g_s|rbu|rbws */
+int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, const float* in0, const float* in1,
+                    int B, int Cin, int H, int W, float* out);
+int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
+
+/* kernel-level entry points (bit-exact tests) */
+int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */
+int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);
+int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out);
+
+/* host entropy coder (compressai-compatible) */
+int mlic_pmf_to_quantized_cdf(const float* pmf, int n, int precision, int32_t* cdf_out /* n + 1 */);
+int mlic_rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const int32_t* cdf,
+                     const int32_t* cdf_len, const int32_t* offset, int n_tables, int stride, uint8_t* out,
+                     size_t cap, size_t* written);
+int mlic_rans_decode(const uint8_t* data, size_t nbytes, const int32_t* indexes, int64_t n, const int32_t* cdf,
+                     const int32_t* cdf_len, const int32_t* offset, int n_tables, int stride, int32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,1 +1,9 @@
-"""mlic_amd: MI355X-native MLIC++ encode/decode (HIP/CDNA4) behind the CompressAI API."""
+"""mlic_amd: MI355X-native (gfx950) MLIC++ encode/decode behind the CompressAI-style API.
+
+    from mlic_amd import get_model
+    net = get_model("MLICPP_L").cuda().eval()
+"""
+from .models import MLICPlusPlus, MLICPlusPlusSD, MLICPlusPlusVbr, get_model, model_config  # noqa: F401
+from .spec import CONFIGS  # noqa: F401
+
+__all__ = ["MLICPlusPlus", "MLICPlusPlusSD", "MLICPlusPlusVbr", "get_model", "model_config", "CONFIGS"]

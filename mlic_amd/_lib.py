@@ -1,0 +1,73 @@
+"""ctypes binding of libmlic_hip.so (C ABI in include/mlic_hip.h).
+
+The library is built in-tree (`python -m mlic_amd.build` or __graft_entry__.build()).  There is no
+fallback: if the shared object is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MLIC_HIP_LIB", os.path.join(_HERE, "libmlic_hip.so"))
+
+_lock = threading.Lock()
+_lib = None
+
+
+class MlicError(RuntimeError):
+    pass
+
+
+def _sig(lib):
+    p, i, i64, f, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
+    P = C.POINTER
+    lib.mlic_last_error.restype = C.c_char_p
+    lib.mlic_version.restype = C.c_char_p
+    sigs = {
+        "mlic_create": [C.c_char_p, i, P(C.c_char_p), P(p), P(i64), P(i), p, P(p)],
+        "mlic_destroy": [p],
+        "mlic_forward": [p, p, p, i, i, i, p, p, p, f],
+        "mlic_set_entropy_tables": [p, p, p, p, i, i, p, p, p, i, i],
+        "mlic_compress": [p, p, p, i, i, i, f],
+        "mlic_encoded_size": [p, i, P(sz), P(sz)],
+        "mlic_encoded_copy": [p, i, p, p],
+        "mlic_encoded_streams": [p, i, P(i64), P(i64), p, p, p],
+        "mlic_decompress": [p, p, P(p), P(sz), P(p), P(sz), i, i, i, p, f],
+        "mlic_run_module": [p, p, C.c_char_p, i, p, p, i, i, i, i, p],
+        "mlic_workspace_bytes": [p, P(sz), P(sz)],
+        "mlic_local_attn_mask": [p, p, i, i],
+        "mlic_image_sq_err_u8": [p, p, p, i, i64, p],
+        "mlic_neglog2_sum": [p, p, i, i64, p],
+        "mlic_pmf_to_quantized_cdf": [p, i, i, p],
+        "mlic_rans_encode": [p, p, i64, p, p, p, i, i, p, sz, P(sz)],
+        "mlic_rans_decode": [p, sz, p, i64, p, p, p, i, i, p],
+    }
+    for name, args in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    return lib
+
+
+def lib():
+    """The loaded library (raises if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise MlicError(f"libmlic_hip.so not found at {LIB_PATH}: build it with "
+                                f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            _lib = _sig(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().mlic_last_error().decode(errors="replace")
+        raise MlicError(f"{what}: {msg}" if what else msg)
+
+
+def call(name: str, *args):
+    check(getattr(lib(), name)(*args), name)

@@ -1,0 +1,188 @@
+// C ABI of libmlic_hip.so (include/mlic_hip.h): status codes, thread-local error text.
+#include "../../include/mlic_hip.h"
+
+#include <cstring>
+#include <string>
+
+#include "model.h"
+
+using namespace mlic;
+
+struct mlic_model {
+  Model* impl;
+};
+
+static thread_local std::string g_err;
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "mlic: unknown error";
+  }
+  return 1;
+}
+
+static CdfTables make_tables(const int32_t* cdf, const int32_t* len, const int32_t* off, int n, int stride) {
+  CdfTables t;
+  t.n = n;
+  t.stride = stride;
+  t.cdf.assign(cdf, cdf + (size_t)n * stride);
+  t.length.assign(len, len + n);
+  t.offset.assign(off, off + n);
+  for (int i = 0; i < n; ++i)
+    MLIC_CHECK(t.length[i] >= 3 && t.length[i] <= stride, "cdf length out of range");
+  return t;
+}
+
+extern "C" {
+
+const char* mlic_last_error(void) { return g_err.c_str(); }
+const char* mlic_version(void) { return "mlic_hip 0.1 gfx950"; }
+
+int mlic_create(const char* model_name, int n, const char* const* names, const float* const* ptrs,
+                const int64_t* shapes, const int* ndims, void* stream, mlic_model** out) {
+  return guard([&] {
+    MLIC_CHECK(out != nullptr, "null out");
+    auto* m = new mlic_model{nullptr};
+    try {
+      m->impl = new Model(model_name, n, names, ptrs, shapes, ndims, (hipStream_t)stream);
+    } catch (...) {
+      delete m;
+      throw;
+    }
+    *out = m;
+  });
+}
+
+int mlic_destroy(mlic_model* m) {
+  return guard([&] {
+    if (!m) return;
+    delete m->impl;
+    delete m;
+  });
+}
+
+int mlic_forward(mlic_model* m, void* stream, const float* x, int B, int H, int W, float* x_hat, float* y_lik,
+                 float* z_lik, float vbr_scale) {
+  return guard([&] {
+    MLIC_CHECK(m && x && B > 0, "bad arguments");
+    m->impl->forward(x, B, H, W, x_hat, y_lik, z_lik, vbr_scale, (hipStream_t)stream);
+  });
+}
+
+int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t* gc_len, const int32_t* gc_off,
+                            int gc_n, int gc_stride, const int32_t* eb_cdf, const int32_t* eb_len,
+                            const int32_t* eb_off, int eb_n, int eb_stride) {
+  return guard([&] {
+    MLIC_CHECK(m, "null model");
+    m->impl->set_tables(make_tables(gc_cdf, gc_len, gc_off, gc_n, gc_stride),
+                        make_tables(eb_cdf, eb_len, eb_off, eb_n, eb_stride));
+  });
+}
+
+int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale) {
+  return guard([&] {
+    MLIC_CHECK(m && x && B > 0, "bad arguments");
+    m->impl->compress(x, B, H, W, vbr_scale, (hipStream_t)stream);
+  });
+}
+
+int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len) {
+  return guard([&] {
+    const EncodedImage& e = m->impl->encoded(b);
+    *y_len = e.y.size();
+    *z_len = e.z.size();
+  });
+}
+
+int mlic_encoded_copy(mlic_model* m, int b, uint8_t* y, uint8_t* z) {
+  return guard([&] {
+    const EncodedImage& e = m->impl->encoded(b);
+    std::memcpy(y, e.y.data(), e.y.size());
+    std::memcpy(z, e.z.data(), e.z.size());
+  });
+}
+
+int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32_t* y_sym, int32_t* y_idx,
+                         int32_t* z_sym) {
+  return guard([&] {
+    const EncodedImage& e = m->impl->encoded(b);
+    *n_y = (int64_t)e.y_sym.size();
+    *n_z = (int64_t)e.z_sym.size();
+    if (y_sym) std::memcpy(y_sym, e.y_sym.data(), e.y_sym.size() * 4);
+    if (y_idx) std::memcpy(y_idx, e.y_idx.data(), e.y_idx.size() * 4);
+    if (z_sym) std::memcpy(z_sym, e.z_sym.data(), e.z_sym.size() * 4);
+  });
+}
+
+int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
+                    const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
+                    float vbr_scale) {
+  return guard([&] {
+    MLIC_CHECK(m && y && z && x_hat && B > 0 && hz > 0 && wz > 0, "bad arguments");
+    m->impl->decompress(y, y_len, z, z_len, B, hz, wz, x_hat, vbr_scale, (hipStream_t)stream);
+  });
+}
+
+int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, const float* in0, const float* in1,
+                    int B, int Cin, int H, int W, float* out) {
+  return guard([&] { m->impl->run_module(which, idx, in0, in1, B, Cin, H, W, out, (hipStream_t)stream); });
+}
+
+int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
+  return guard([&] {
+    *arena = m->impl->arena_bytes();
+    *weights = m->impl->weight_bytes();
+  });
+}
+
+int mlic_local_attn_mask(void* stream, float* out, int H, int W) {
+  return guard([&] { local_mask(out, H, W, (hipStream_t)stream); });
+}
+
+int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out) {
+  return guard([&] { sq_err_u8(a, n_per, b, n_per, out, n_per, B, (hipStream_t)stream); });
+}
+
+int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out) {
+  return guard([&] {
+    HIP_OK(hipMemsetAsync(out, 0, sizeof(double) * B, (hipStream_t)stream));
+    neglog2_sum(lik, n_per, B, out, (hipStream_t)stream);
+  });
+}
+
+int mlic_pmf_to_quantized_cdf(const float* pmf, int n, int precision, int32_t* cdf_out) {
+  return guard([&] {
+    auto c = pmf_to_quantized_cdf(pmf, n, precision);
+    for (size_t i = 0; i < c.size(); ++i) cdf_out[i] = (int32_t)c[i];
+  });
+}
+
+int mlic_rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const int32_t* cdf,
+                     const int32_t* cdf_len, const int32_t* offset, int n_tables, int stride, uint8_t* out,
+                     size_t cap, size_t* written) {
+  return guard([&] {
+    CdfTables t = make_tables(cdf, cdf_len, offset, n_tables, stride);
+    std::string s = rans_encode(symbols, indexes, n, t);
+    *written = s.size();
+    MLIC_CHECK(s.size() <= cap, "output buffer too small");
+    std::memcpy(out, s.data(), s.size());
+  });
+}
+
+int mlic_rans_decode(const uint8_t* data, size_t nbytes, const int32_t* indexes, int64_t n, const int32_t* cdf,
+                     const int32_t* cdf_len, const int32_t* offset, int n_tables, int stride, int32_t* out) {
+  return guard([&] {
+    CdfTables t = make_tables(cdf, cdf_len, offset, n_tables, stride);
+    RansDecoderState d;
+    d.set_stream(data, nbytes);
+    d.decode(indexes, n, t, out);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+// Host-side launchers of the MLIC++ HIP kernels (see conv_mfma.hip, kernels.hip).
+#pragma once
+#include "common.h"
+
+namespace mlic {
+
+// implicit-GEMM conv on MFMA (conv_mfma.hip)
+void conv_forward(const ConvParams& P, hipStream_t st);
+
+struct DwParams {
+  Seg seg[MAXSEG];
+  int nseg;
+  int C, H, W, Ho, Wo, stride;
+  const float* w;     // [C][9]
+  const float* bias;  // [C]
+  float* out;
+  int64_t out_bs;
+  int gelu;
+  int B;
+};
+void dw3x3(const DwParams& P, hipStream_t st);
+
+void ln_channels(const float* x, int64_t x_bs, float* y, int64_t y_bs, const float* g, const float* b, int C,
+                 int HW, int B, hipStream_t st);
+
+struct LocalAttnParams {
+  const float* qkv;
+  int64_t qkv_bs;
+  float* out;  // [C*25][HW]
+  int64_t out_bs;
+  const float* rel_table;  // [81][2]
+  const int* rel_index;    // [625] int32
+  float scale;
+  int C, H, W, B;
+};
+void local_attn(const LocalAttnParams& P, hipStream_t st);
+
+void softmax_spatial(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int mask_mode,
+                     hipStream_t st);
+void softmax_channel(const float* x, int64_t x_bs, float* y, int64_t y_bs, int heads, int hd, int H, int W, int B,
+                     int mask_mode, hipStream_t st);
+void linear_attention(const float* K, int64_t k_bs, const float* V, int64_t v_bs, const float* Q, int64_t q_bs,
+                      float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int HW, int B,
+                      int nsplit, hipStream_t st);
+void ckbd_mask(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int keep_anchor,
+               hipStream_t st);
+
+struct QuantParams {
+  const float* y;  // latent slice [C][HW] (encoder side)
+  int64_t y_bs;
+  const float* params;  // EP output of this phase [2C][HW]
+  int64_t params_bs;
+  const float* params_a;  // anchor-phase EP output (likelihood merge), phase 1 only
+  int64_t params_a_bs;
+  float* yh;  // y_hat slice [C][HW]
+  int64_t yh_bs;
+  float* lik;  // likelihood slice or null
+  int64_t lik_bs;
+  int32_t* sym;  // squeezed symbols or null
+  int32_t* idx;  // squeezed indexes or null
+  const float* table;
+  int ntable;
+  int phase;  // 0 anchor, 1 non-anchor
+  int vbr;
+  float sc, rs;
+  int C, H, W, B;
+};
+void quant_phase(const QuantParams& P, hipStream_t st);
+void phase_indexes(const QuantParams& P, hipStream_t st);
+void phase_dequant(const QuantParams& P, hipStream_t st);
+
+struct EbParams {
+  const float* z;
+  float* z_hat;
+  float* lik;
+  int32_t* sym;
+  const float* quantiles;  // [C][1][3]
+  const float *m0, *m1, *m2, *m3, *m4;
+  const float *b0, *b1, *b2, *b3, *b4;
+  const float *f0, *f1, *f2, *f3;
+  int C, H, W, B;
+};
+void eb_forward(const EbParams& P, hipStream_t st);
+void eb_dequant(const int32_t* sym, const float* quantiles, float* z_hat, int C, int HW, int B, hipStream_t st);
+
+void pack_conv(const float* w, float* out, int Cout, int Cin, int KK, hipStream_t st);
+void gdn_prep(const float* beta, const float* gamma, const float* bb, const float* bped, const float* gb,
+              const float* gped, float* beta_eff, float* gamma_pk, int C, hipStream_t st);
+void local_mask(float* out, int H, int W, hipStream_t st);
+void sq_err_u8(const float* a, int64_t a_bs, const float* b, int64_t b_bs, double* out, int64_t n_per, int B,
+               hipStream_t st);
+void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, hipStream_t st);
+
+}  // namespace mlic

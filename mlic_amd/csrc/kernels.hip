@@ -1,0 +1,717 @@
+// Bandwidth-bound and small-reduction kernels of the MLIC++ hot path (gfx950).
+//
+//  dw3x3 ............ DepthWiseConv's depthwise half (conv.py:46-63), stride 1/2, LDS halo tile,
+//                     multi-segment (channel-concat) input, optional GELU
+//  ln_channels ...... nn.LayerNorm over channels of an NCHW map (context.py:73, 110)
+//  local_attn ....... LocalContext windowed 5x5 attention (context.py:75-107): q/k/v halo tile in
+//                     LDS, Swin relative-position bias, checkerboard mask computed from parity bits
+//  softmax_spatial .. F.softmax(keys, dim=L) (context.py:180, 235), optional anchor-only support
+//  softmax_channel .. F.softmax(queries, dim=head channels) (context.py:181, 236)
+//  ctx_partial/reduce K.V^T over L as a split reduction with a fixed-order combine
+//  attn_apply ....... ctx^T . Q (context.py:187, 239)
+//  quant / likelihood / indexes / dequant: ste_round, GaussianConditional, build_indexes,
+//                     checkerboard phases (mlicpp.py:112-138, ckbd.py:123-220)
+//  eb_forward ....... EntropyBottleneck factorized likelihood + median rounding (compressai)
+#include "common.h"
+#include "kernels.h"
+
+namespace mlic {
+
+// =============================================================================================
+// depthwise 3x3, pad 1
+constexpr int DW_TW = 64, DW_TH = 8;
+
+__global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
+  __shared__ float tile[(DW_TH * 2 + 2) * (DW_TW * 2 + 2)];
+  const int s = P.stride;
+  const int tw_in = DW_TW * s + 2, th_in = DW_TH * s + 2;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const int ntx = (P.Wo + DW_TW - 1) / DW_TW;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int ox0 = tx * DW_TW, oy0 = ty * DW_TH;
+  const int ix0 = ox0 * s - 1, iy0 = oy0 * s - 1;
+  // segment lookup
+  int sg = 0, c0 = 0;
+  while (sg + 1 < P.nseg && c >= c0 + P.seg[sg].C) { c0 += P.seg[sg].C; ++sg; }
+  const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
+  for (int i = threadIdx.x; i < tw_in * th_in; i += 256) {
+    const int yy = i / tw_in, xx = i - yy * tw_in;
+    const int gy = iy0 + yy, gx = ix0 + xx;
+    tile[i] = (gy >= 0 && gy < P.H && gx >= 0 && gx < P.W) ? src[(int64_t)gy * P.W + gx] : 0.0f;
+  }
+  __syncthreads();
+  float w[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w[k] = P.w[c * 9 + k];
+  const float bias = P.bias ? P.bias[c] : 0.0f;
+  float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)c * P.Ho * P.Wo;
+  for (int i = threadIdx.x; i < DW_TW * DW_TH; i += 256) {
+    const int ly = i / DW_TW, lx = i - ly * DW_TW;
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    if (oy >= P.Ho || ox >= P.Wo) continue;
+    const float* t = tile + (ly * s) * tw_in + lx * s;
+    float acc = 0.0f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], t[ky * tw_in + kx], acc);
+    float v = acc + bias;
+    if (P.gelu) v = gelu_erf(v);
+    dst[(int64_t)oy * P.Wo + ox] = v;
+  }
+}
+
+void dw3x3(const DwParams& P, hipStream_t st) {
+  MLIC_CHECK(P.stride == 1 || P.stride == 2, "dw stride");
+  MLIC_CHECK(P.Ho == (P.H - 1) / P.stride + 1 && P.Wo == (P.W - 1) / P.stride + 1, "dw output size");
+  int tot = 0;
+  for (int i = 0; i < P.nseg; ++i) tot += P.seg[i].C;
+  MLIC_CHECK(tot == P.C, "dw segments");
+  const int ntx = (P.Wo + DW_TW - 1) / DW_TW, nty = (P.Ho + DW_TH - 1) / DW_TH;
+  hipLaunchKernelGGL(dw3x3_kernel, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// LayerNorm over C channels of each pixel (C <= 128), NCHW
+template <int C>
+__global__ void ln_channels_kernel(const float* __restrict__ x, int64_t x_bs, float* __restrict__ y, int64_t y_bs,
+                                   const float* __restrict__ g, const float* __restrict__ bta, int HW, float eps) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (p >= HW) return;
+  const float* xp = x + (int64_t)b * x_bs + p;
+  float v[C];
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) { v[c] = xp[(int64_t)c * HW]; s += v[c]; }
+  const float mean = s / (float)C;
+  float q = 0.0f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) { const float d = v[c] - mean; q = fmaf(d, d, q); }
+  const float rstd = 1.0f / sqrtf(q / (float)C + eps);
+  float* yp = y + (int64_t)b * y_bs + p;
+#pragma unroll
+  for (int c = 0; c < C; ++c) yp[(int64_t)c * HW] = (v[c] - mean) * rstd * g[c] + bta[c];
+}
+
+void ln_channels(const float* x, int64_t x_bs, float* y, int64_t y_bs, const float* g, const float* b, int C,
+                 int HW, int B, hipStream_t st) {
+  const dim3 grid((HW + 127) / 128, B);
+  if (C == 32) hipLaunchKernelGGL(ln_channels_kernel<32>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, g, b, HW, 1e-5f);
+  else if (C == 64) hipLaunchKernelGGL(ln_channels_kernel<64>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, g, b, HW, 1e-5f);
+  else if (C == 128) hipLaunchKernelGGL(ln_channels_kernel<128>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, g, b, HW, 1e-5f);
+  else MLIC_CHECK(false, "LayerNorm channels must be 32, 64 or 128");
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// LocalContext windowed attention.  qkv: [B][3C][H*W] (q = ch [0,C), k = [C,2C), v = [2C,3C)),
+// output T: [B][C*25][H*W] with row = (head*hd + d)*25 + query_cell, which is exactly the
+// (c', ky, kx) flattening the 5x5 "fusion" conv contracts over.
+constexpr int LA_T = 8;                 // 8x8 positions per workgroup
+constexpr int LA_HALO = LA_T + 4;       // 12x12 staged cells
+
+template <int HD>
+__global__ __launch_bounds__(256) void local_attn_kernel(LocalAttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int C = 2 * HD, hd = HD;
+  const int H = P.H, W = P.W, HW = H * W;
+  const int b = blockIdx.y;
+  const int ntx = (W + LA_T - 1) / LA_T;
+  const int x0 = (blockIdx.x % ntx) * LA_T, y0 = (blockIdx.x / ntx) * LA_T;
+  // stage qkv halo: sm[ch][cell], ch in [0, 3C), cell in [0, 144); zero outside the image
+  const float* src = P.qkv + (int64_t)b * P.qkv_bs;
+  constexpr int NCELL = LA_HALO * LA_HALO;
+  for (int i = threadIdx.x; i < 3 * C * NCELL; i += 256) {
+    const int ch = i / NCELL, cell = i - ch * NCELL;
+    const int gy = y0 - 2 + cell / LA_HALO, gx = x0 - 2 + cell % LA_HALO;
+    sm[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? src[(int64_t)ch * HW + gy * W + gx] : 0.0f;
+  }
+  float* bias_s = sm + 3 * C * NCELL;  // [2][25][25]
+  for (int i = threadIdx.x; i < 2 * 625; i += 256) {
+    const int h = i / 625, ij = i - h * 625;
+    bias_s[i] = P.rel_table[P.rel_index[ij] * 2 + h];
+  }
+  __syncthreads();
+  const float* qs = sm;
+  const float* ks = sm + C * NCELL;
+  const float* vs = sm + 2 * C * NCELL;
+  const float scale = P.scale;
+  // work items: (query cell i, head h, local position) with position fastest
+  for (int item = threadIdx.x; item < 25 * 2 * LA_T * LA_T; item += 256) {
+    const int pl = item % (LA_T * LA_T);
+    const int hh = (item / (LA_T * LA_T)) & 1;
+    const int qi = item / (2 * LA_T * LA_T);
+    const int ly = pl / LA_T, lx = pl % LA_T;
+    const int py = y0 + ly, px = x0 + lx;
+    if (py >= H || px >= W) continue;
+    const int qky = qi / 5, qkx = qi % 5;
+    const int qcell = (ly + qky) * LA_HALO + (lx + qkx);
+    const int qgy = py + qky - 2, qgx = px + qkx - 2;
+    const bool q_anchor = qgy >= 0 && qgy < H && qgx >= 0 && qgx < W && (((qgy + qgx) & 1) == 1);
+    float qv[HD];
+#pragma unroll
+    for (int d = 0; d < hd; ++d) qv[d] = qs[(d * 2 + hh) * NCELL + qcell] * scale;
+    float sc[25];
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int j = 0; j < 25; ++j) {
+      const int kcell = (ly + j / 5) * LA_HALO + (lx + j % 5);
+      float dot = 0.0f;
+#pragma unroll
+      for (int d = 0; d < hd; ++d) dot = fmaf(qv[d], ks[(d * 2 + hh) * NCELL + kcell], dot);
+      const int kgy = py + j / 5 - 2, kgx = px + j % 5 - 2;
+      const bool k_anchor = kgy >= 0 && kgy < H && kgx >= 0 && kgx < W && (((kgy + kgx) & 1) == 1);
+      float s = dot + bias_s[hh * 625 + qi * 25 + j];
+      s = s + ((q_anchor && k_anchor) ? 0.0f : -100.0f);
+      sc[j] = s;
+      mx = fmaxf(mx, s);
+    }
+    float sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 25; ++j) { sc[j] = expf(sc[j] - mx); sum += sc[j]; }
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int j = 0; j < 25; ++j) sc[j] = sc[j] * inv;
+    float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)py * W + px;
+    for (int d = 0; d < hd; ++d) {
+      float o = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 25; ++j) {
+        const int kcell = (ly + j / 5) * LA_HALO + (lx + j % 5);
+        o = fmaf(sc[j], vs[(d * 2 + hh) * NCELL + kcell], o);
+      }
+      dst[(int64_t)((hh * hd + d) * 25 + qi) * HW] = o;
+    }
+  }
+}
+
+void local_attn(const LocalAttnParams& P, hipStream_t st) {
+  MLIC_CHECK(P.C % 2 == 0 && P.C / 2 <= 32, "local attention head dim");
+  const size_t lds = (size_t)(3 * P.C * LA_HALO * LA_HALO + 2 * 625) * sizeof(float);
+  MLIC_CHECK(lds <= 160 * 1024, "local attention LDS");
+  const int ntx = (P.W + LA_T - 1) / LA_T, nty = (P.H + LA_T - 1) / LA_T;
+  if (P.C == 32) hipLaunchKernelGGL(local_attn_kernel<16>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  else if (P.C == 64) hipLaunchKernelGGL(local_attn_kernel<32>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  else MLIC_CHECK(false, "LocalContext dim must be 32 or 64");
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// softmax over the spatial axis of each (b, channel) row; mask_mode 1 => only anchor positions
+// participate (others output 0): the intra-slice "keys" over the squeezed anchor half.
+__global__ __launch_bounds__(256) void softmax_spatial_kernel(const float* __restrict__ x, int64_t x_bs,
+                                                              float* __restrict__ y, int64_t y_bs, int H, int W,
+                                                              int mask_mode) {
+  __shared__ float red[256];
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int HW = H * W;
+  const float* xr = x + (int64_t)b * x_bs + (int64_t)c * HW;
+  float* yr = y + (int64_t)b * y_bs + (int64_t)c * HW;
+  auto active = [&](int p) { return mask_mode == 0 || is_anchor(p / W, p % W); };
+  float mx = -3.0e38f;
+  for (int p = threadIdx.x; p < HW; p += 256)
+    if (active(p)) mx = fmaxf(mx, xr[p]);
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  mx = red[0];
+  __syncthreads();
+  float sum = 0.0f;
+  for (int p = threadIdx.x; p < HW; p += 256)
+    if (active(p)) sum += expf(xr[p] - mx);
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const float inv = 1.0f / red[0];
+  for (int p = threadIdx.x; p < HW; p += 256) yr[p] = active(p) ? expf(xr[p] - mx) * inv : 0.0f;
+}
+
+void softmax_spatial(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int mask_mode,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(softmax_spatial_kernel, dim3(C, B), dim3(256), 0, st, x, x_bs, y, y_bs, H, W, mask_mode);
+  HIP_OK(hipGetLastError());
+}
+
+// softmax over the hd channels of each head at each pixel; mask_mode 2 => output only at
+// non-anchor pixels (intra-slice queries), 0 elsewhere
+template <int HD>
+__global__ void softmax_channel_kernel(const float* __restrict__ x, int64_t x_bs, float* __restrict__ y,
+                                       int64_t y_bs, int heads, int H, int W, int mask_mode) {
+  constexpr int hd = HD;
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int h = blockIdx.y % heads, b = blockIdx.y / heads;
+  if (p >= HW) return;
+  const float* xp = x + (int64_t)b * x_bs + (int64_t)h * hd * HW + p;
+  float* yp = y + (int64_t)b * y_bs + (int64_t)h * hd * HW + p;
+  if (mask_mode == 2 && is_anchor(p / W, p % W)) {
+    for (int d = 0; d < hd; ++d) yp[(int64_t)d * HW] = 0.0f;
+    return;
+  }
+  float v[HD];
+  float mx = -3.0e38f;
+#pragma unroll
+  for (int d = 0; d < hd; ++d) { v[d] = xp[(int64_t)d * HW]; mx = fmaxf(mx, v[d]); }
+  float sum = 0.0f;
+#pragma unroll
+  for (int d = 0; d < hd; ++d) { v[d] = expf(v[d] - mx); sum += v[d]; }
+  const float inv = 1.0f / sum;
+#pragma unroll
+  for (int d = 0; d < hd; ++d) yp[(int64_t)d * HW] = v[d] * inv;
+}
+
+void softmax_channel(const float* x, int64_t x_bs, float* y, int64_t y_bs, int heads, int hd, int H, int W, int B,
+                     int mask_mode, hipStream_t st) {
+  const dim3 grid((H * W + 127) / 128, heads * B);
+  if (hd == 16) hipLaunchKernelGGL(softmax_channel_kernel<16>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, heads, H, W, mask_mode);
+  else if (hd == 32) hipLaunchKernelGGL(softmax_channel_kernel<32>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, heads, H, W, mask_mode);
+  else MLIC_CHECK(false, "head dim must be 16 or 32");
+  HIP_OK(hipGetLastError());
+}
+
+// ctx[b][h][c][d] = sum_p K[b][h*hd+c][p] * V[b][h*hd+d][p], split over NSPLIT chunks of p,
+// partials combined in a fixed order by ctx_reduce (bitwise reproducible, no atomics)
+constexpr int CTX_CHUNK = 64;
+
+__global__ __launch_bounds__(256) void ctx_partial_kernel(const float* __restrict__ K, int64_t k_bs,
+                                                          const float* __restrict__ V, int64_t v_bs,
+                                                          float* __restrict__ part, int heads, int hd, int HW,
+                                                          int nsplit) {
+  __shared__ float ks[32][CTX_CHUNK + 1];
+  __shared__ float vs[32][CTX_CHUNK + 1];
+  const int split = blockIdx.x, h = blockIdx.y % heads, b = blockIdx.y / heads;
+  const int per = (HW + nsplit - 1) / nsplit;
+  const int pbeg = split * per, pend = min(HW, pbeg + per);
+  const float* kb = K + (int64_t)b * k_bs + (int64_t)h * hd * HW;
+  const float* vb = V + (int64_t)b * v_bs + (int64_t)h * hd * HW;
+  const int nout = hd * hd;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int p0 = pbeg; p0 < pend; p0 += CTX_CHUNK) {
+    for (int i = threadIdx.x; i < hd * CTX_CHUNK; i += 256) {
+      const int c = i / CTX_CHUNK, pp = i % CTX_CHUNK;
+      const int p = p0 + pp;
+      ks[c][pp] = p < pend ? kb[(int64_t)c * HW + p] : 0.0f;
+      vs[c][pp] = p < pend ? vb[(int64_t)c * HW + p] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = threadIdx.x + r * 256;
+      if (o < nout) {
+        const int c = o / hd, d = o % hd;
+        float a = acc[r];
+        for (int pp = 0; pp < CTX_CHUNK; ++pp) a = fmaf(ks[c][pp], vs[d][pp], a);
+        acc[r] = a;
+      }
+    }
+    __syncthreads();
+  }
+  float* dst = part + (((int64_t)b * heads + h) * nsplit + split) * nout;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = threadIdx.x + r * 256;
+    if (o < nout) dst[o] = acc[r];
+  }
+}
+
+__global__ void ctx_reduce_kernel(const float* __restrict__ part, float* __restrict__ ctx, int nout, int nsplit,
+                                  int total) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over (b*heads) * nout
+  if (i >= total) return;
+  const int bh = i / nout, o = i % nout;
+  const float* src = part + (int64_t)bh * nsplit * nout + o;
+  float s = 0.0f;
+  for (int k = 0; k < nsplit; ++k) s += src[(int64_t)k * nout];
+  ctx[i] = s;
+}
+
+// out[b][h*hd+d][p] = sum_c ctx[b][h][c][d] * Q[b][h*hd+c][p]
+template <int HD>
+__global__ __launch_bounds__(256) void attn_apply_kernel(const float* __restrict__ ctx, const float* __restrict__ Q,
+                                                         int64_t q_bs, float* __restrict__ out, int64_t o_bs,
+                                                         int heads, int HW) {
+  constexpr int hd = HD;
+  __shared__ float cs[32 * 32];
+  const int h = blockIdx.y % heads, b = blockIdx.y / heads;
+  const float* cb = ctx + ((int64_t)b * heads + h) * hd * hd;
+  for (int i = threadIdx.x; i < hd * hd; i += 256) cs[i] = cb[i];
+  __syncthreads();
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= HW) return;
+  const float* qp = Q + (int64_t)b * q_bs + (int64_t)h * hd * HW + p;
+  float q[HD];
+#pragma unroll
+  for (int c = 0; c < hd; ++c) q[c] = qp[(int64_t)c * HW];
+  float* op = out + (int64_t)b * o_bs + (int64_t)h * hd * HW + p;
+  for (int d = 0; d < hd; ++d) {
+    float a = 0.0f;
+#pragma unroll
+    for (int c = 0; c < hd; ++c) a = fmaf(cs[c * hd + d], q[c], a);
+    op[(int64_t)d * HW] = a;
+  }
+}
+
+void linear_attention(const float* K, int64_t k_bs, const float* V, int64_t v_bs, const float* Q, int64_t q_bs,
+                      float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int HW, int B,
+                      int nsplit, hipStream_t st) {
+  MLIC_CHECK(hd == 16 || hd == 32, "head dim");
+  hipLaunchKernelGGL(ctx_partial_kernel, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads, hd,
+                     HW, nsplit);
+  HIP_OK(hipGetLastError());
+  const int total = B * heads * hd * hd;
+  hipLaunchKernelGGL(ctx_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, ctx, hd * hd, nsplit,
+                     total);
+  HIP_OK(hipGetLastError());
+  if (hd == 16)
+    hipLaunchKernelGGL(attn_apply_kernel<16>, dim3((HW + 255) / 256, heads * B), dim3(256), 0, st, ctx, Q, q_bs, out,
+                       o_bs, heads, HW);
+  else
+    hipLaunchKernelGGL(attn_apply_kernel<32>, dim3((HW + 255) / 256, heads * B), dim3(256), 0, st, ctx, Q, q_bs, out,
+                       o_bs, heads, HW);
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// checkerboard mask copy (ckbd_anchor / ckbd_nonanchor as a materialised map)
+__global__ void ckbd_mask_kernel(const float* __restrict__ x, int64_t x_bs, float* __restrict__ y, int64_t y_bs, int C,
+                                 int H, int W, int keep_anchor) {
+  const int64_t HW = (int64_t)H * W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= C * HW) return;
+  const int p = (int)(i % HW);
+  const bool a = is_anchor(p / W, p % W);
+  y[(int64_t)b * y_bs + i] = (a == (keep_anchor != 0)) ? x[(int64_t)b * x_bs + i] : 0.0f;
+}
+
+void ckbd_mask(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int keep_anchor,
+               hipStream_t st) {
+  const int64_t n = (int64_t)C * H * W;
+  hipLaunchKernelGGL(ckbd_mask_kernel, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, st, x, x_bs, y, y_bs, C, H,
+                     W, keep_anchor);
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// slice-loop quantisation.  params: EP output [2C] (scales = [0,C), means = [C,2C)).
+//  phase 0 (anchor):     yh[c,p] = anchor(p) ? q(y, m) : 0
+//  phase 1 (non-anchor): yh[c,p] = anchor(p) ? yh[c,p] : q(y, m_na);  and, when lik != null,
+//                        lik[c,p] = GC(y, s_sel, m_sel) with (s,m) taken from pa at anchor pixels
+//                        and from pn at non-anchor pixels (ckbd_merge).
+//  q(y, m) = round((y - m) * sc) * rs + m  (sc = rs = 1 => exactly torch.round(y - m) + m)
+//  sym/idx (optional): int32 squeezed [C][H][W/2] phase streams for the rANS coder.
+__device__ __forceinline__ float std_cum(float x) { return 0.5f * erfcf(-0.70710678118654752440f * x); }
+
+__device__ __forceinline__ float gauss_lik(float y, float s, float m) {
+  // compressai GaussianConditional.forward (eval): dequantize, _likelihood, lower bounds
+  const float outv = rintf(y - m) + m;
+  const float v = fabsf(outv - m);
+  const float sb = fmaxf(s, 0.11f);
+  const float lik = std_cum((0.5f - v) / sb) - std_cum((-0.5f - v) / sb);
+  return fmaxf(lik, 1e-9f);
+}
+
+__device__ __forceinline__ int scale_index(float s, const float* __restrict__ table, int n) {
+  // compressai build_indexes: (n - 1) - #{t in table[:-1] : max(s, 0.11) <= t}
+  const float sb = fmaxf(s, 0.11f);
+  int idx = n - 1;
+  for (int k = 0; k < n - 1; ++k) idx -= (sb <= table[k]) ? 1 : 0;
+  return idx;
+}
+
+__global__ void quant_phase_kernel(QuantParams P) {
+  const int HW = P.H * P.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= (int64_t)P.C * HW) return;
+  const int c = (int)(i / HW), p = (int)(i % HW);
+  const int h = p / P.W, w = p % P.W;
+  const bool anc = is_anchor(h, w);
+  const bool mine = (P.phase == 0) == anc;
+  const float y = P.y[(int64_t)b * P.y_bs + i];
+  const float* pp = P.params + (int64_t)b * P.params_bs;
+  float* yh = P.yh + (int64_t)b * P.yh_bs + i;
+  if (P.lik) {
+    const float* pa = P.params_a + (int64_t)b * P.params_a_bs;
+    const float s = anc ? pa[(int64_t)c * HW + p] : pp[(int64_t)c * HW + p];
+    const float m = anc ? pa[(int64_t)(c + P.C) * HW + p] : pp[(int64_t)(c + P.C) * HW + p];
+    float lk;
+    if (P.vbr) lk = gauss_lik(y * P.sc, s * P.sc, m * P.sc);
+    else lk = gauss_lik(y, s, m);
+    P.lik[(int64_t)b * P.lik_bs + i] = lk;
+  }
+  if (!mine) {
+    if (P.phase == 0) *yh = 0.0f;
+    return;
+  }
+  const float s = pp[(int64_t)c * HW + p];
+  const float m = pp[(int64_t)(c + P.C) * HW + p];
+  float q;
+  if (P.vbr) q = rintf((y - m) * P.sc);
+  else q = rintf(y - m);
+  *yh = P.vbr ? q * P.rs + m : q + m;
+  if (P.sym) {
+    const int64_t sq = (int64_t)b * P.C * HW / 2 + ((int64_t)c * P.H + h) * (P.W / 2) + (w >> 1);
+    P.sym[sq] = (int32_t)q;
+    P.idx[sq] = scale_index(P.vbr ? s * P.sc : s, P.table, P.ntable);
+  }
+}
+
+void quant_phase(const QuantParams& P, hipStream_t st) {
+  MLIC_CHECK(P.W % 2 == 0, "even latent width");
+  const int64_t n = (int64_t)P.C * P.H * P.W;
+  hipLaunchKernelGGL(quant_phase_kernel, dim3((unsigned)((n + 255) / 256), P.B), dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// decoder: indexes of one phase (squeezed order), from the EP scales
+__global__ void phase_indexes_kernel(QuantParams P) {
+  const int HW = P.H * P.W, W2 = P.W / 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // squeezed index within image
+  const int b = blockIdx.y;
+  if (i >= (int64_t)P.C * P.H * W2) return;
+  const int c = (int)(i / (P.H * W2));
+  const int r = (int)(i % (P.H * W2));
+  const int h = r / W2, j = r % W2;
+  const int w = 2 * j + ((P.phase == 0) ? (1 - (h & 1)) : (h & 1));
+  const float s = P.params[(int64_t)b * P.params_bs + (int64_t)c * HW + h * P.W + w];
+  P.idx[(int64_t)b * P.C * P.H * W2 + i] = scale_index(P.vbr ? s * P.sc : s, P.table, P.ntable);
+}
+
+void phase_indexes(const QuantParams& P, hipStream_t st) {
+  const int64_t n = (int64_t)P.C * P.H * (P.W / 2);
+  hipLaunchKernelGGL(phase_indexes_kernel, dim3((unsigned)((n + 255) / 256), P.B), dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// decoder: yh at the phase's pixels = sym * rs + m (anchor phase also zeroes the others)
+__global__ void phase_dequant_kernel(QuantParams P) {
+  const int HW = P.H * P.W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= (int64_t)P.C * HW) return;
+  const int c = (int)(i / HW), p = (int)(i % HW);
+  const int h = p / P.W, w = p % P.W;
+  const bool mine = (P.phase == 0) == is_anchor(h, w);
+  float* yh = P.yh + (int64_t)b * P.yh_bs + i;
+  if (!mine) {
+    if (P.phase == 0) *yh = 0.0f;
+    return;
+  }
+  const int64_t sq = (int64_t)b * P.C * HW / 2 + ((int64_t)c * P.H + h) * (P.W / 2) + (w >> 1);
+  const float q = (float)P.sym[sq];
+  const float m = P.params[(int64_t)b * P.params_bs + (int64_t)(c + P.C) * HW + p];
+  *yh = P.vbr ? q * P.rs + m : q + m;
+}
+
+void phase_dequant(const QuantParams& P, hipStream_t st) {
+  const int64_t n = (int64_t)P.C * P.H * P.W;
+  hipLaunchKernelGGL(phase_dequant_kernel, dim3((unsigned)((n + 255) / 256), P.B), dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// EntropyBottleneck: z_hat = round(z - med) + med, likelihood via the factorized logistic
+// cumulative (filters 3,3,3,3), symbols = round(z - med) for the coder
+__device__ __forceinline__ float softplus_t(float x) {
+  // F.softplus(beta=1, threshold=20)
+  return x > 20.0f ? x : log1pf(expf(x));
+}
+
+__device__ void eb_logits(const EbParams& P, int c, float x, float* out1) {
+  float v[3];
+  float u[3];
+  // layer 0: [3x1]
+  for (int o = 0; o < 3; ++o) {
+    float a = softplus_t(P.m0[c * 3 + o]) * x;
+    a = a + P.b0[c * 3 + o];
+    a = a + tanhf(P.f0[c * 3 + o]) * tanhf(a);
+    v[o] = a;
+  }
+  const float* ms[3] = {P.m1, P.m2, P.m3};
+  const float* bs[3] = {P.b1, P.b2, P.b3};
+  const float* fs[3] = {P.f1, P.f2, P.f3};
+  for (int l = 0; l < 3; ++l) {
+    for (int o = 0; o < 3; ++o) {
+      float a = 0.0f;
+      for (int k = 0; k < 3; ++k) a = fmaf(softplus_t(ms[l][(c * 3 + o) * 3 + k]), v[k], a);
+      a = a + bs[l][c * 3 + o];
+      a = a + tanhf(fs[l][c * 3 + o]) * tanhf(a);
+      u[o] = a;
+    }
+    for (int o = 0; o < 3; ++o) v[o] = u[o];
+  }
+  float a = 0.0f;
+  for (int k = 0; k < 3; ++k) a = fmaf(softplus_t(P.m4[c * 3 + k]), v[k], a);
+  *out1 = a + P.b4[c];
+}
+
+__global__ void eb_forward_kernel(EbParams P) {
+  const int HW = P.H * P.W;
+  const int64_t n = (int64_t)P.B * P.C * HW;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)((i / HW) % P.C);
+  const float med = P.quantiles[c * 3 + 1];
+  const float z = P.z[i];
+  const float r = rintf(z - med);
+  const float zh = r + med;
+  if (P.z_hat) P.z_hat[i] = zh;
+  if (P.sym) P.sym[i] = (int32_t)r;
+  if (P.lik) {
+    float lo, up;
+    eb_logits(P, c, zh - 0.5f, &lo);
+    eb_logits(P, c, zh + 0.5f, &up);
+    const float sl = 1.0f / (1.0f + expf(-lo));
+    const float su = 1.0f / (1.0f + expf(-up));
+    P.lik[i] = fmaxf(su - sl, 1e-9f);
+  }
+}
+
+void eb_forward(const EbParams& P, hipStream_t st) {
+  const int64_t n = (int64_t)P.B * P.C * P.H * P.W;
+  hipLaunchKernelGGL(eb_forward_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// z_hat from decoded symbols (decoder side)
+__global__ void eb_dequant_kernel(const int32_t* __restrict__ sym, const float* __restrict__ quantiles,
+                                  float* __restrict__ z_hat, int C, int HW, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)((i / HW) % C);
+  z_hat[i] = (float)sym[i] + quantiles[c * 3 + 1];
+}
+
+void eb_dequant(const int32_t* sym, const float* quantiles, float* z_hat, int C, int HW, int B, hipStream_t st) {
+  const int64_t n = (int64_t)B * C * HW;
+  hipLaunchKernelGGL(eb_dequant_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sym, quantiles, z_hat, C,
+                     HW, n);
+  HIP_OK(hipGetLastError());
+}
+
+// =============================================================================================
+// weight preparation (model create time)
+// conv weight [Cout][Cin][K][K] (or linear [Cout][Cin]) -> packed [K*K][Cin][Cout]
+__global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict__ out, int Cout, int Cin, int KK) {
+  const int64_t n = (int64_t)Cout * Cin * KK;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int co = (int)(i / ((int64_t)Cin * KK));
+  const int rem = (int)(i % ((int64_t)Cin * KK));
+  const int ci = rem / KK, tap = rem % KK;
+  out[((int64_t)tap * Cin + ci) * Cout + co] = w[i];
+}
+
+void pack_conv(const float* w, float* out, int Cout, int Cin, int KK, hipStream_t st) {
+  const int64_t n = (int64_t)Cout * Cin * KK;
+  hipLaunchKernelGGL(pack_conv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, out, Cout, Cin, KK);
+  HIP_OK(hipGetLastError());
+}
+
+// GDN reparametrisation: eff = max(p, bound)^2 - pedestal; gamma [C][C] is packed as a 1x1 conv
+__global__ void gdn_prep_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
+                                const float* __restrict__ bb, const float* __restrict__ bped,
+                                const float* __restrict__ gb, const float* __restrict__ gped,
+                                float* __restrict__ beta_eff, float* __restrict__ gamma_pk, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < C) {
+    const float v = fmaxf(beta[i], bb[0]);
+    beta_eff[i] = v * v - bped[0];
+  }
+  if (i < C * C) {
+    const int co = i / C, ci = i % C;
+    const float v = fmaxf(gamma[i], gb[0]);
+    gamma_pk[ci * C + co] = v * v - gped[0];
+  }
+}
+
+void gdn_prep(const float* beta, const float* gamma, const float* bb, const float* bped, const float* gb,
+              const float* gped, float* beta_eff, float* gamma_pk, int C, hipStream_t st) {
+  hipLaunchKernelGGL(gdn_prep_kernel, dim3((C * C + 255) / 256), dim3(256), 0, st, beta, gamma, bb, bped, gb, gped,
+                     beta_eff, gamma_pk, C);
+  HIP_OK(hipGetLastError());
+}
+
+// LocalContext attention mask as the reference materialises it (for the bit-exact test only;
+// the attention kernel derives it from parity bits)
+__global__ void local_mask_kernel(float* __restrict__ out, int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)H * W * 625;
+  if (i >= n) return;
+  const int p = (int)(i / 625), ij = (int)(i % 625);
+  const int qi = ij / 25, kj = ij % 25;
+  const int py = p / W, px = p % W;
+  auto va = [&](int cell) {
+    const int y = py + cell / 5 - 2, x = px + cell % 5 - 2;
+    return y >= 0 && y < H && x >= 0 && x < W && (((y + x) & 1) == 1);
+  };
+  out[i] = (va(qi) && va(kj)) ? 0.0f : -100.0f;
+}
+
+void local_mask(float* out, int H, int W, hipStream_t st) {
+  const int64_t n = (int64_t)H * W * 625;
+  hipLaunchKernelGGL(local_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, H, W);
+  HIP_OK(hipGetLastError());
+}
+
+// image metrics support: uint8 truncation as torchvision ToPILImage (clamp, *255, .byte())
+__global__ void sq_err_u8_kernel(const float* __restrict__ a, const float* __restrict__ b, double* __restrict__ out,
+                                 int64_t n_per, int64_t a_bs, int64_t b_bs) {
+  __shared__ double red[256];
+  const int img = blockIdx.y;
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_per; i += (int64_t)gridDim.x * 256) {
+    const float va = floorf(fminf(fmaxf(a[img * a_bs + i], 0.0f), 1.0f) * 255.0f);
+    const float vb = floorf(fminf(fmaxf(b[img * b_bs + i], 0.0f), 1.0f) * 255.0f);
+    const double d = (double)va - (double)vb;
+    s += d * d;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(out + img, red[0]);
+}
+
+void sq_err_u8(const float* a, int64_t a_bs, const float* b, int64_t b_bs, double* out, int64_t n_per, int B,
+               hipStream_t st) {
+  HIP_OK(hipMemsetAsync(out, 0, sizeof(double) * B, st));
+  const int nb = (int)std::min<int64_t>(1024, (n_per + 255) / 256);
+  hipLaunchKernelGGL(sq_err_u8_kernel, dim3(nb, B), dim3(256), 0, st, a, b, out, n_per, a_bs, b_bs);
+  HIP_OK(hipGetLastError());
+}
+
+// sum of log2 likelihoods per image (bpp numerator): per-block partial sums in a fixed order
+__global__ void neglog2_sum_kernel(const float* __restrict__ lik, int64_t n_per, double* __restrict__ out) {
+  __shared__ double red[256];
+  const int img = blockIdx.y;
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_per; i += (int64_t)gridDim.x * 256)
+    s += -(double)log2f(lik[img * n_per + i]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(out + img, red[0]);
+}
+
+void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, hipStream_t st) {
+  const int nb = (int)std::min<int64_t>(256, (n_per + 255) / 256);
+  hipLaunchKernelGGL(neglog2_sum_kernel, dim3(nb, B), dim3(256), 0, st, lik, n_per, out);
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace mlic

@@ -1,0 +1,900 @@
+// MLIC++ executor.  Every method cites the reference code it re-expresses; the arithmetic runs in
+// the HIP kernels (conv_mfma.hip, kernels.hip), this file only wires views, weights and phases.
+#include "model.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace mlic {
+
+// ------------------------------------------------------------------------------------- configs
+Cfg config_for(const std::string& name) {  // config/config.py:19-62 (+ MLICPP_L_VBR)
+  Cfg c;
+  c.name = name;
+  if (name == "MLICPP_L" || name == "MLICPP_L_VBR") { c.N = 192; c.M = 320; c.S = 10; }
+  else if (name == "MLICPP_S" || name == "MLICPP_S_VBR") { c.N = 96; c.M = 160; c.S = 5; }
+  else if (name == "MLICPP_M") { c.N = 160; c.M = 256; c.S = 8; }
+  else if (name == "MLICPP_S2") { c.N = 128; c.M = 128; c.S = 2; }
+  else if (name == "MLICPP_M_SMALL_DEC") { c.N = 192; c.M = 320; c.S = 10; c.sd = true; }
+  else throw Error("mlic: unknown model name " + name);
+  c.vbr = name.size() > 4 && name.substr(name.size() - 4) == "_VBR";
+  c.C = c.M / c.S;
+  return c;
+}
+
+// ------------------------------------------------------------------------------------- arena
+Arena::~Arena() {
+  if (base_) (void)hipFree(base_);
+}
+
+void Arena::ensure(size_t bytes) {
+  if (bytes <= cap_) return;
+  if (base_) HIP_OK(hipFree(base_));
+  base_ = nullptr;
+  HIP_OK(hipMalloc(&base_, bytes));
+  cap_ = bytes;
+}
+
+float* Arena::alloc(int64_t nfloats) {
+  const size_t bytes = ((size_t)nfloats * sizeof(float) + 255) & ~(size_t)255;
+  const size_t off = top_;
+  top_ += bytes;
+  peak_ = std::max(peak_, top_);
+  if (dry_) return reinterpret_cast<float*>((uintptr_t)0x1000 + off);  // never dereferenced
+  MLIC_CHECK(top_ <= cap_, "arena overflow (plan mismatch)");
+  return reinterpret_cast<float*>(base_ + off);
+}
+
+// ------------------------------------------------------------------------------------- weights
+static bool ends_with(const std::string& s, const std::string& t) {
+  return s.size() >= t.size() && s.compare(s.size() - t.size(), t.size(), t) == 0;
+}
+
+Model::Model(const std::string& name, int n, const char* const* names, const float* const* ptrs,
+             const int64_t* shapes, const int* ndims, hipStream_t st)
+    : cfg_(config_for(name)) {
+  // one owned device block for every weight (packed or copied)
+  std::vector<int64_t> numel(n);
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    int64_t e = 1;
+    for (int d = 0; d < ndims[i]; ++d) e *= shapes[i * 4 + d];
+    numel[i] = e;
+    total += ((size_t)e * 4 + 255) & ~(size_t)255;
+  }
+  for (int i = 0; i < n; ++i)
+    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(numel[i] + shapes[i * 4]) * 4 + 512;
+  total += 64 * 4 + 625 * 4 + 1024;
+  char* block = nullptr;
+  HIP_OK(hipMalloc(&block, total));
+  owned_.push_back(block);
+  wbytes_ = total;
+  size_t off = 0;
+  auto take = [&](int64_t nf) {
+    char* p = block + off;
+    off += ((size_t)nf * 4 + 255) & ~(size_t)255;
+    return reinterpret_cast<float*>(p);
+  };
+  std::map<std::string, int> idx;
+  for (int i = 0; i < n; ++i) idx[names[i]] = i;
+  auto shape = [&](int i, int d) { return (int)shapes[i * 4 + d]; };
+
+  for (int i = 0; i < n; ++i) {
+    const std::string k = names[i];
+    float* dst = take(numel[i]);
+    const std::string base = k.substr(0, k.rfind('.'));
+    if (ends_with(k, ".weight") && ndims[i] == 4 && shape(i, 1) == 1 && shape(i, 0) > 1) {
+      // depthwise [C,1,3,3]
+      HIP_OK(hipMemcpyAsync(dst, ptrs[i], numel[i] * 4, hipMemcpyDeviceToDevice, st));
+      DwW w;
+      w.w = dst;
+      w.C = shape(i, 0);
+      MLIC_CHECK(shape(i, 2) == 3 && shape(i, 3) == 3, "depthwise kernels are 3x3");
+      dws_[base] = w;
+    } else if (ends_with(k, ".weight") && (ndims[i] == 4 || ndims[i] == 2) &&
+               k.find("entropy_bottleneck") == std::string::npos && k.find("norm") == std::string::npos) {
+      ConvW w;
+      w.w = dst;
+      w.Cout = shape(i, 0);
+      if (ndims[i] == 2) {  // nn.Linear == 1x1 conv
+        w.Cin = shape(i, 1);
+        w.K = 1;
+      } else if (k.find("local_context") != std::string::npos && ends_with(k, ".fusion.weight")) {
+        // 5x5 valid conv over the 5x5 window tensor == 1x1 conv over Cin*25 rows (c*25 + cell)
+        w.Cin = shape(i, 1) * shape(i, 2) * shape(i, 3);
+        w.K = 1;
+      } else {
+        w.Cin = shape(i, 1);
+        w.K = shape(i, 2);
+        MLIC_CHECK(shape(i, 2) == shape(i, 3), "square kernels only");
+      }
+      pack_conv(ptrs[i], dst, w.Cout, w.Cin, w.K * w.K, st);
+      convs_[base] = w;
+    } else {
+      HIP_OK(hipMemcpyAsync(dst, ptrs[i], numel[i] * 4, hipMemcpyDeviceToDevice, st));
+      raw_[k] = dst;
+    }
+  }
+  // biases
+  for (auto& kv : convs_) {
+    auto it = raw_.find(kv.first + ".bias");
+    if (it != raw_.end()) kv.second.b = it->second;
+  }
+  for (auto& kv : dws_) {
+    auto it = raw_.find(kv.first + ".bias");
+    if (it != raw_.end()) kv.second.b = it->second;
+  }
+  // GDN: eff = max(p, bound)^2 - pedestal; gamma as a 1x1 conv with beta_eff as its bias
+  for (int i = 0; i < n; ++i) {
+    const std::string k = names[i];
+    if (!ends_with(k, ".gamma") || ndims[i] != 2) continue;
+    const std::string p = k.substr(0, k.size() - 6);
+    const int C = shape(i, 0);
+    float* beta_eff = take(C);
+    float* gamma_pk = take((int64_t)C * C);
+    MLIC_CHECK(off <= total, "weight block");
+    gdn_prep(rw(p + ".beta"), rw(p + ".gamma"), rw(p + ".beta_reparam.lower_bound.bound"),
+             rw(p + ".beta_reparam.pedestal"), rw(p + ".gamma_reparam.lower_bound.bound"),
+             rw(p + ".gamma_reparam.pedestal"), beta_eff, gamma_pk, C, st);
+    ConvW w;
+    w.w = gamma_pk;
+    w.b = beta_eff;
+    w.Cin = w.Cout = C;
+    w.K = 1;
+    convs_[p + ".__gdn"] = w;
+  }
+  MLIC_CHECK(off <= total, "weight block overflow");
+  // relative position index (attention.py:28-39), int32
+  {
+    const int win = cfg_.win, ww = win * win;
+    std::vector<int> ri(ww * ww);
+    for (int a = 0; a < ww; ++a)
+      for (int c = 0; c < ww; ++c)
+        ri[a * ww + c] = (a / win - c / win + win - 1) * (2 * win - 1) + (a % win - c % win + win - 1);
+    rel_index_ = reinterpret_cast<int*>(take(ww * ww));
+    HIP_OK(hipMemcpyAsync(rel_index_, ri.data(), ri.size() * 4, hipMemcpyHostToDevice, st));
+  }
+  MLIC_CHECK(raw_.count("__scale_table"), "scale table missing");
+  scale_table_ = const_cast<float*>(raw_["__scale_table"]);
+  HIP_OK(hipStreamSynchronize(st));
+}
+
+Model::~Model() {
+  for (void* p : owned_) (void)hipFree(p);
+  if (h_sym_) (void)hipHostFree(h_sym_);
+  if (h_idx_) (void)hipHostFree(h_idx_);
+}
+
+const ConvW& Model::cw(const std::string& k) const {
+  auto it = convs_.find(k);
+  if (it == convs_.end()) throw Error("mlic: missing conv weight " + k);
+  return it->second;
+}
+const DwW& Model::dww(const std::string& k) const {
+  auto it = dws_.find(k);
+  if (it == dws_.end()) throw Error("mlic: missing depthwise weight " + k);
+  return it->second;
+}
+const float* Model::rw(const std::string& k) const {
+  auto it = raw_.find(k);
+  if (it == raw_.end()) throw Error("mlic: missing tensor " + k);
+  return it->second;
+}
+
+// ------------------------------------------------------------------------------------- blocks
+View Model::alloc(int C, int H, int W) {
+  View v;
+  v.p = arena_.alloc((int64_t)B_ * C * H * W);
+  v.C = C;
+  v.H = H;
+  v.W = W;
+  v.bs = (int64_t)C * H * W;
+  return v;
+}
+
+void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
+                 const View* aux, const View* res) {
+  ConvParams P{};
+  MLIC_CHECK(!ins.empty() && (int)ins.size() <= MAXSEG, "conv inputs");
+  P.nseg = (int)ins.size();
+  int cin = 0;
+  for (int s = 0; s < P.nseg; ++s) {
+    MLIC_CHECK(ins[s].H == ins[0].H && ins[s].W == ins[0].W, "concat inputs must share H, W");
+    P.seg[s] = {ins[s].p, ins[s].C, ins[s].bs};
+    cin += ins[s].C;
+  }
+  MLIC_CHECK(cin == w.Cin, "conv Cin mismatch");
+  P.Cin = cin;
+  P.H = ins[0].H;
+  P.W = ins[0].W;
+  P.Cout = w.Cout;
+  P.K = w.K;
+  P.stride = stride;
+  P.pad = pad;
+  P.Ho = (P.H + 2 * pad - w.K) / stride + 1;
+  P.Wo = (P.W + 2 * pad - w.K) / stride + 1;
+  P.wpk = w.w;
+  P.bias = w.b;
+  P.epi = epi;
+  if (epi & EPI_SHUFFLE) {
+    MLIC_CHECK(out.C * 4 == w.Cout && out.H == 2 * P.Ho && out.W == 2 * P.Wo, "shuffle output shape");
+  } else {
+    MLIC_CHECK(out.C == w.Cout && out.H == P.Ho && out.W == P.Wo, "conv output shape");
+  }
+  P.out = out.p;
+  P.out_bs = out.bs;
+  P.out_cs = out.hw();
+  if (aux) {
+    MLIC_CHECK(aux->C == w.Cout && aux->H == P.Ho && aux->W == P.Wo, "aux shape");
+    P.aux = aux->p;
+    P.aux_bs = aux->bs;
+  }
+  if (res) {
+    MLIC_CHECK(res->C == out.C && res->H == out.H && res->W == out.W, "residual shape");
+    P.res = res->p;
+    P.res_bs = res->bs;
+    P.epi |= EPI_RES;
+  }
+  P.B = B_;
+  if (!dry_) conv_forward(P, st_);
+}
+
+void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {
+  DwParams P{};
+  P.nseg = (int)ins.size();
+  int c = 0;
+  for (int s = 0; s < P.nseg; ++s) {
+    P.seg[s] = {ins[s].p, ins[s].C, ins[s].bs};
+    c += ins[s].C;
+  }
+  MLIC_CHECK(c == w.C && out.C == w.C, "depthwise channels");
+  P.C = c;
+  P.H = ins[0].H;
+  P.W = ins[0].W;
+  P.stride = stride;
+  P.Ho = (P.H - 1) / stride + 1;
+  P.Wo = (P.W - 1) / stride + 1;
+  MLIC_CHECK(out.H == P.Ho && out.W == P.Wo, "depthwise output shape");
+  P.w = w.w;
+  P.bias = w.b;
+  P.out = out.p;
+  P.out_bs = out.bs;
+  P.gelu = gelu ? 1 : 0;
+  P.B = B_;
+  if (!dry_) dw3x3(P, st_);
+}
+
+// conv3x3 of the fork (modules/layers/conv.py:22-32): DepthWiseConv (dw 3x3 -> pw 1x1) by default,
+// compressai's dense 3x3 for the *_old modules.  `epi` applies to the last (pointwise) conv.
+View Model::conv3x3(const std::vector<View>& ins, const std::string& p, int stride, bool dwsep, int epi,
+                    const View* res, const View* out_opt) {
+  const int H = ins[0].H, W = ins[0].W;
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  if (!dwsep) {
+    const ConvW& w = cw(p);
+    View out = out_opt ? *out_opt : alloc(w.Cout, Ho, Wo);
+    conv(ins, w, stride, 1, out, epi, nullptr, res);
+    return out;
+  }
+  const DwW& d = dww(p + ".depth_conv");
+  const ConvW& w = cw(p + ".point_conv");
+  View out = out_opt ? *out_opt : alloc(w.Cout, Ho, Wo);
+  const size_t m = arena_.mark();
+  View t = alloc(d.C, Ho, Wo);
+  dw(ins, d, stride, t, false);
+  conv({t}, w, 1, 0, out, epi, nullptr, res);
+  arena_.release(m);
+  return out;
+}
+
+View Model::conv1x1(const View& in, const std::string& p, int stride, int epi, const View* res) {
+  const ConvW& w = cw(p);
+  View out = alloc(w.Cout, (in.H - 1) / stride + 1, (in.W - 1) / stride + 1);
+  conv({in}, w, stride, 0, out, epi, nullptr, res);
+  return out;
+}
+
+// compressai GDN: out = x * rsqrt(conv2d(x^2, gamma, beta)) (inverse: * sqrt)
+void Model::gdn(const View& x, const std::string& p, bool inverse, const View& out, const View* res) {
+  conv({x}, cw(p + ".__gdn"), 1, 0, out, EPI_SQUARE_IN | (inverse ? EPI_IGDN : EPI_GDN), &x, res);
+}
+
+// res_blk.py:62-93 ResidualBlockWithStride
+View Model::rbws(const View& x, const std::string& p, bool dwsep) {
+  const int Ho = (x.H - 1) / 2 + 1, Wo = (x.W - 1) / 2 + 1;
+  const ConvW& sk = cw(p + ".skip");
+  View out = alloc(sk.Cout, Ho, Wo);
+  const size_t m = arena_.mark();
+  View t1 = conv3x3({x}, p + ".conv1", 2, dwsep, EPI_GELU);
+  View t2 = conv3x3({t1}, p + ".conv2", 1, dwsep, EPI_NONE);
+  View s = alloc(sk.Cout, Ho, Wo);
+  conv({x}, sk, 2, 0, s, EPI_NONE);
+  gdn(t2, p + ".gdn", false, out, &s);
+  arena_.release(m);
+  return out;
+}
+
+// res_blk.py:124-154 ResidualBlock: out = gelu(conv2(gelu(conv1(x)))) + (skip(x) or x)
+View Model::rb(const View& x, const std::string& p, bool dwsep) {
+  const bool has_skip = convs_.count(p + ".skip") > 0;
+  const int Cout = dwsep ? cw(p + ".conv2.point_conv").Cout : cw(p + ".conv2").Cout;
+  View out = alloc(Cout, x.H, x.W);
+  const size_t m = arena_.mark();
+  View t1 = conv3x3({x}, p + ".conv1", 1, dwsep, EPI_GELU);
+  View id = x;
+  if (has_skip) {
+    id = alloc(Cout, x.H, x.W);
+    conv({x}, cw(p + ".skip"), 1, 0, id, EPI_NONE);
+  }
+  conv3x3({t1}, p + ".conv2", 1, dwsep, EPI_GELU, &id, &out);
+  arena_.release(m);
+  return out;
+}
+
+// res_blk.py:96-121 ResidualBlockUpsample: igdn(dwsep(gelu(subpel(x)))) + subpel_up(x)
+View Model::rbu(const View& x, const std::string& p) {
+  const ConvW& a = cw(p + ".subpel_conv.0");
+  const ConvW& u = cw(p + ".upsample.0");
+  const int C = a.Cout / 4;
+  View out = alloc(C, 2 * x.H, 2 * x.W);
+  const size_t m = arena_.mark();
+  View ta = alloc(C, 2 * x.H, 2 * x.W);
+  conv({x}, a, 1, 1, ta, EPI_GELU | EPI_SHUFFLE);
+  View tu = alloc(C, 2 * x.H, 2 * x.W);
+  conv({x}, u, 1, 1, tu, EPI_SHUFFLE);
+  View tc = conv3x3({ta}, p + ".conv", 1, true, EPI_NONE);
+  gdn(tc, p + ".igdn", true, out, &tu);
+  arena_.release(m);
+  return out;
+}
+
+// analysis.py:6-22 (SD: analysis_old with dense 3x3)
+View Model::g_a(const View& x) {
+  const bool dwsep = !cfg_.sd;
+  const std::string g = "g_a.analysis_transform";
+  const int M = cfg_.M;
+  View y = alloc(M, (x.H + 15) / 16, (x.W + 15) / 16);
+  const size_t m = arena_.mark();
+  View a = rbws(x, g + ".0", dwsep);
+  View b = rb(a, g + ".1", dwsep);
+  View c = rbws(b, g + ".2", dwsep);
+  View d = rb(c, g + ".3", dwsep);
+  View e = rbws(d, g + ".4", dwsep);
+  View f = rb(e, g + ".5", dwsep);
+  conv3x3({f}, g + ".6", 2, dwsep, EPI_NONE, nullptr, &y);
+  arena_.release(m);
+  return y;
+}
+
+// analysis.py:25-48
+View Model::h_a(const View& y) {
+  const bool dwsep = !cfg_.sd;
+  const std::string h = "h_a.reduction";
+  View z = alloc(cfg_.N, (y.H + 3) / 4, (y.W + 3) / 4);
+  const size_t m = arena_.mark();
+  View a = conv3x3({y}, h + ".0", 1, dwsep, EPI_GELU);
+  View b = conv3x3({a}, h + ".2", 1, dwsep, EPI_GELU);
+  View c = conv3x3({b}, h + ".4", 2, dwsep, EPI_GELU);
+  View d = conv3x3({c}, h + ".6", 1, dwsep, EPI_GELU);
+  conv3x3({d}, h + ".8", 2, dwsep, EPI_NONE, nullptr, &z);
+  arena_.release(m);
+  return z;
+}
+
+// synthesis.py:9-33
+View Model::h_s(const View& z) {
+  const std::string h = "h_s.increase";
+  const int hM = cfg_.hM();
+  View out = alloc(2 * hM, 4 * z.H, 4 * z.W);
+  const size_t m = arena_.mark();
+  View a = conv3x3({z}, h + ".0", 1, true, EPI_GELU);
+  View b = alloc(hM, 2 * z.H, 2 * z.W);
+  conv({a}, cw(h + ".2.0"), 1, 1, b, EPI_GELU | EPI_SHUFFLE);
+  View c = conv3x3({b}, h + ".4", 1, true, EPI_GELU);
+  View d = alloc(hM * 3 / 2, 4 * z.H, 4 * z.W);
+  conv({c}, cw(h + ".6.0"), 1, 1, d, EPI_GELU | EPI_SHUFFLE);
+  conv3x3({d}, h + ".8", 1, true, EPI_NONE, nullptr, &out);
+  arena_.release(m);
+  return out;
+}
+
+// synthesis.py:56-73
+void Model::g_s(const View& yh, const View& out) {
+  const std::string g = "g_s.synthesis_transform";
+  const size_t m = arena_.mark();
+  View a = rb(yh, g + ".0", true);
+  View b = rbu(a, g + ".1");
+  View c = rb(b, g + ".2", true);
+  View d = rbu(c, g + ".3");
+  View e = rb(d, g + ".4", true);
+  View f = rbu(e, g + ".5");
+  View h = rb(f, g + ".6", true);
+  conv({h}, cw(g + ".7.0"), 1, 1, out, EPI_SHUFFLE);
+  arena_.release(m);
+}
+
+// ------------------------------------------------------------------------------------- MEM++
+// context.py:67-112 LocalContext
+View Model::local_context(const View& x, int i) {
+  const std::string p = "local_context." + std::to_string(i);
+  const int C = x.C, H = x.H, W = x.W;
+  View out = alloc(2 * C, H, W);
+  const size_t m = arena_.mark();
+  View n1 = alloc(C, H, W);
+  if (!dry_) ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, B_, st_);
+  View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
+  View t = alloc(25 * C, H, W);
+  if (!dry_) {
+    LocalAttnParams A{};
+    A.qkv = qkv.p;
+    A.qkv_bs = qkv.bs;
+    A.out = t.p;
+    A.out_bs = t.bs;
+    A.rel_table = rw(p + ".relative_position_table");
+    A.rel_index = rel_index_;
+    A.scale = (float)std::pow((double)(C / 2), -0.5);  // context.py:27 head_dim ** -0.5
+    A.C = C;
+    A.H = H;
+    A.W = W;
+    A.B = B_;
+    local_attn(A, st_);
+  }
+  View f = conv1x1(t, p + ".fusion", 1, EPI_NONE);
+  View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
+  View n2 = alloc(2 * C, H, W);
+  if (!dry_)
+    ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, B_, st_);
+  View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
+  conv({h1}, cw(p + ".mlp.fc2"), 1, 0, out, EPI_NONE, nullptr, &pj);
+  arena_.release(m);
+  return out;
+}
+
+// context.py:115-138 ChannelContext (SD: context_old, dense 3x3)
+View Model::channel_context(const View& x, int i) {
+  const std::string p = "channel_context." + std::to_string(i) + ".fushion";
+  const bool dwsep = !cfg_.sd;
+  const int Cout = dwsep ? cw(p + ".4.point_conv").Cout : cw(p + ".4").Cout;
+  View out = alloc(Cout, x.H, x.W);
+  const size_t m = arena_.mark();
+  View a = conv3x3({x}, p + ".0", 1, dwsep, EPI_GELU);
+  View b = conv3x3({a}, p + ".2", 1, dwsep, EPI_GELU);
+  conv3x3({b}, p + ".4", 1, dwsep, EPI_NONE, nullptr, &out);
+  arena_.release(m);
+  return out;
+}
+
+// nn.Sequential(conv1x1, depthwise 3x3) of keys/queries/values
+View Model::qkv_branch(const View& x, const std::string& p) {
+  const DwW& d = dww(p + ".1");
+  View out = alloc(d.C, x.H, x.W);
+  const size_t m = arena_.mark();
+  View t = conv1x1(x, p + ".0", 1, EPI_NONE);
+  dw({t}, d, 1, out, false);
+  arena_.release(m);
+  return out;
+}
+
+static int ctx_splits(int HW) { return std::max(1, std::min(64, HW / 256)); }
+
+// context.py:195-245 LinearGlobalInterContext
+View Model::inter_context(const View& x, int i) {
+  const std::string p = "global_inter_context." + std::to_string(i);
+  const int D = x.C, H = x.H, W = x.W, HW = H * W;
+  const int heads = D / 32, hd = 32;  // num_heads = slice_ch * i // 32 (mlicpp.py:50)
+  const ConvW& sk = cw(p + ".skip");
+  View out = alloc(sk.Cout, H, W);
+  const size_t m = arena_.mark();
+  View q = qkv_branch(x, p + ".queries");
+  View k = qkv_branch(x, p + ".keys");
+  View v = qkv_branch(x, p + ".values");
+  View ks = alloc(D, H, W);
+  View qs = alloc(D, H, W);
+  View att = alloc(D, H, W);
+  const int nsplit = ctx_splits(HW);
+  float* part = arena_.alloc((int64_t)B_ * heads * nsplit * hd * hd);
+  float* ctx = arena_.alloc((int64_t)B_ * heads * hd * hd);
+  if (!dry_) {
+    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, B_, 0, st_);
+    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, B_, 0, st_);
+    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, B_, nsplit, st_);
+  }
+  const ConvW& rp = cw(p + ".reprojection");
+  View a = alloc(rp.Cout, H, W);
+  conv({att}, rp, 1, 2, a, EPI_NONE);
+  View m1 = conv1x1(a, p + ".mlp.0", 1, EPI_GELU);
+  View m2 = alloc(m1.C, H, W);
+  dw({m1}, dww(p + ".mlp.2"), 1, m2, true);
+  View s = conv1x1(a, p + ".skip", 1, EPI_NONE);
+  conv({m2}, cw(p + ".mlp.4"), 1, 0, out, EPI_NONE, nullptr, &s);
+  arena_.release(m);
+  return out;
+}
+
+// context.py:140-193 LinearGlobalIntraContext: q from non-anchor cells of x1, k from anchor cells of
+// x1, v from x2; the squeezed-half softmaxes are computed on the full grid with parity masks.
+View Model::intra_context(const View& x1, const View& x2, int i) {
+  const std::string p = "global_intra_context." + std::to_string(i);
+  const int D = x1.C, H = x1.H, W = x1.W, HW = H * W;
+  const int heads = 2, hd = D / 2;
+  View out = alloc(2 * D, H, W);
+  const size_t m = arena_.mark();
+  View x1n = alloc(D, H, W);
+  View x1a = alloc(D, H, W);
+  if (!dry_) {
+    ckbd_mask(x1.p, x1.bs, x1n.p, x1n.bs, D, H, W, B_, 0, st_);
+    ckbd_mask(x1.p, x1.bs, x1a.p, x1a.bs, D, H, W, B_, 1, st_);
+  }
+  View q = qkv_branch(x1n, p + ".queries");
+  View k = qkv_branch(x1a, p + ".keys");
+  View v = qkv_branch(x2, p + ".values");
+  View ks = alloc(D, H, W);
+  View qs = alloc(D, H, W);
+  View att = alloc(D, H, W);
+  const int nsplit = ctx_splits(HW);
+  float* part = arena_.alloc((int64_t)B_ * heads * nsplit * hd * hd);
+  float* ctx = arena_.alloc((int64_t)B_ * heads * hd * hd);
+  if (!dry_) {
+    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, B_, 1, st_);
+    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, B_, 2, st_);
+    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, B_, nsplit, st_);
+  }
+  const ConvW& rp = cw(p + ".reprojection");
+  View a = alloc(rp.Cout, H, W);
+  conv({att}, rp, 1, 2, a, EPI_NONE);
+  View m1 = conv1x1(a, p + ".mlp.0", 1, EPI_GELU);
+  View m2 = alloc(m1.C, H, W);
+  dw({m1}, dww(p + ".mlp.2"), 1, m2, true);
+  conv({m2}, cw(p + ".mlp.4"), 1, 0, out, EPI_NONE, nullptr, &a);
+  arena_.release(m);
+  return out;
+}
+
+// entropy.py:7-29
+View Model::entropy_parameters(const std::vector<View>& ins, const std::string& kind, int i) {
+  const std::string p = "entropy_parameters_" + kind + "." + std::to_string(i) + ".fusion";
+  const int H = ins[0].H, W = ins[0].W;
+  const ConvW& l3 = cw(p + ".6");
+  View out = alloc(l3.Cout, H, W);
+  const size_t m = arena_.mark();
+  View a = alloc(cw(p + ".0").Cout, H, W);
+  conv(ins, cw(p + ".0"), 1, 0, a, EPI_GELU);
+  View b = conv1x1(a, p + ".2", 1, EPI_GELU);
+  View c = conv1x1(b, p + ".4", 1, EPI_GELU);
+  conv({c}, l3, 1, 0, out, EPI_NONE);
+  arena_.release(m);
+  return out;
+}
+
+// quantization.py:30-44 (SD: LatentResidualPredictionOld, 4 layers); the last conv's epilogue
+// applies 0.5*tanh, the checkerboard mask and the residual add into the y_hat slice in place
+// (mlicpp.py:119-120, 137-138).
+void Model::lrp(const std::vector<View>& ins, const std::string& kind, int i, const View& yh, bool anchor) {
+  const std::string p = "lrp_" + kind + "." + std::to_string(i) + ".lrp_transform";
+  const int nl = cfg_.sd ? 4 : 3;
+  const size_t m = arena_.mark();
+  std::vector<View> cur = ins;
+  for (int l = 0; l < nl; ++l) {
+    const std::string q = p + "." + std::to_string(2 * l);
+    if (l + 1 < nl) {
+      View o = conv3x3(cur, q, 1, true, EPI_GELU);
+      cur = {o};
+    } else {
+      const int epi = EPI_TANH_HALF | (anchor ? EPI_MASK_ANCHOR : EPI_MASK_NONANCHOR);
+      conv3x3(cur, q, 1, true, epi, &yh, &yh);
+    }
+  }
+  arena_.release(m);
+}
+
+// ------------------------------------------------------------------------------------- phases
+class PhaseDecoder {
+ public:
+  PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym, int32_t* h_idx)
+      : t_(t), h_sym_(h_sym), h_idx_(h_idx) {
+    dec_.resize(B);
+    for (int b = 0; b < B; ++b) dec_[b].set_stream(y[b], ylen[b]);
+  }
+  void run(int64_t n_per, hipStream_t st, int32_t* d_idx, int32_t* d_sym) {
+    const int B = (int)dec_.size();
+    HIP_OK(hipMemcpyAsync(h_idx_, d_idx, sizeof(int32_t) * n_per * B, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    auto work = [&](int b) { dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per); };
+    if (B == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int b = 0; b < B; ++b) th.emplace_back(work, b);
+      for (auto& x : th) x.join();
+    }
+    HIP_OK(hipMemcpyAsync(d_sym, h_sym_, sizeof(int32_t) * n_per * B, hipMemcpyHostToDevice, st));
+  }
+
+ private:
+  std::vector<RansDecoderState> dec_;
+  const CdfTables* t_;
+  int32_t* h_sym_;
+  int32_t* h_idx_;
+};
+
+// mlicpp.py:107-176 (forward), 220-277 (compress), 309-366 (decompress)
+void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, int32_t* d_sym,
+                       int32_t* d_idx, PhaseDecoder* dec) {
+  const int S = cfg_.S, C = cfg_.C, hM = cfg_.hM();
+  const int H = hyper.H, W = hyper.W, HW = H * W;
+  const int64_t n_per = (int64_t)C * H * (W / 2);
+  const View hyper_means = hyper.ch(hM, hM);
+  for (int idx = 0; idx < S; ++idx) {
+    const size_t m = arena_.mark();
+    View ysl = yhat.ch(idx * C, C);
+    View inter, chan, pa;
+    if (idx == 0) {
+      pa = entropy_parameters({hyper}, "anchor", 0);
+    } else {
+      View prev = yhat.ch(0, idx * C);
+      inter = inter_context(prev, idx);
+      chan = channel_context(prev, idx);
+      pa = entropy_parameters({inter, chan, hyper}, "anchor", idx);
+    }
+    for (int ph = 0; ph < 2; ++ph) {
+      QuantParams Q{};
+      Q.C = C;
+      Q.H = H;
+      Q.W = W;
+      Q.B = B_;
+      Q.yh = ysl.p;
+      Q.yh_bs = ysl.bs;
+      Q.table = scale_table_;
+      Q.ntable = 64;
+      Q.vbr = vbr_on_ ? 1 : 0;
+      Q.sc = vbr_sc_;
+      Q.rs = vbr_rs_;
+      Q.phase = ph;
+      View pn;
+      if (ph == 1) {
+        View local = local_context(ysl, idx);
+        if (idx == 0) {
+          pn = entropy_parameters({local, hyper}, "nonanchor", 0);
+        } else {
+          View intra = intra_context(yhat.ch((idx - 1) * C, C), ysl, idx);
+          pn = entropy_parameters({local, intra, inter, chan, hyper}, "nonanchor", idx);
+        }
+      }
+      const View& par = ph == 0 ? pa : pn;
+      Q.params = par.p;
+      Q.params_bs = par.bs;
+      const int phase_id = 2 * idx + ph;
+      if (mode == Mode::Decode) {
+        int32_t* di = d_idx;
+        int32_t* ds = d_sym;
+        Q.idx = di;
+        Q.sym = ds;
+        if (!dry_) {
+          phase_indexes(Q, st_);
+          dec->run(n_per, st_, di, ds);
+          phase_dequant(Q, st_);
+        }
+      } else {
+        Q.y = y->p + (int64_t)idx * C * HW;
+        Q.y_bs = y->bs;
+        if (ph == 1 && mode == Mode::Forward && y_lik) {
+          Q.lik = y_lik + (int64_t)idx * C * HW;
+          Q.lik_bs = (int64_t)cfg_.M * HW;
+          Q.params_a = pa.p;
+          Q.params_a_bs = pa.bs;
+        }
+        if (mode == Mode::Encode) {
+          Q.sym = d_sym + (int64_t)phase_id * B_ * n_per;
+          Q.idx = d_idx + (int64_t)phase_id * B_ * n_per;
+        }
+        if (!dry_) quant_phase(Q, st_);
+      }
+      // LRP on cat([hyper_means] + y_hat_slices + [current])
+      lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
+    }
+    arena_.release(m);
+  }
+}
+
+void Model::eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym) {
+  if (dry_) return;
+  EbParams P{};
+  const std::string p = "entropy_bottleneck";
+  P.z = z.p;
+  P.z_hat = z_hat.p;
+  P.lik = z_lik;
+  P.sym = z_sym;
+  P.quantiles = rw(p + ".quantiles");
+  P.m0 = rw(p + "._matrix0"); P.m1 = rw(p + "._matrix1"); P.m2 = rw(p + "._matrix2");
+  P.m3 = rw(p + "._matrix3"); P.m4 = rw(p + "._matrix4");
+  P.b0 = rw(p + "._bias0"); P.b1 = rw(p + "._bias1"); P.b2 = rw(p + "._bias2");
+  P.b3 = rw(p + "._bias3"); P.b4 = rw(p + "._bias4");
+  P.f0 = rw(p + "._factor0"); P.f1 = rw(p + "._factor1"); P.f2 = rw(p + "._factor2"); P.f3 = rw(p + "._factor3");
+  P.C = z.C;
+  P.H = z.H;
+  P.W = z.W;
+  P.B = B_;
+  eb_forward(P, st_);
+}
+
+template <class F>
+void Model::planned(int B, hipStream_t st, F&& body) {
+  B_ = B;
+  st_ = st;
+  dry_ = true;
+  arena_.begin(true);
+  body();
+  const size_t need = arena_.peak();
+  dry_ = false;
+  arena_.ensure(need + (1 << 20));
+  arena_.begin(false);
+  body();
+}
+
+void Model::ensure_host(size_t n) {
+  if (n <= h_cap_) return;
+  if (h_sym_) HIP_OK(hipHostFree(h_sym_));
+  if (h_idx_) HIP_OK(hipHostFree(h_idx_));
+  HIP_OK(hipHostMalloc(&h_sym_, n * sizeof(int32_t)));
+  HIP_OK(hipHostMalloc(&h_idx_, n * sizeof(int32_t)));
+  h_cap_ = n;
+}
+
+// ------------------------------------------------------------------------------------- entry points
+void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
+                    hipStream_t st) {
+  MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64 (pad like utils/testing.py:130-137)");
+  vbr_on_ = cfg_.vbr;
+  vbr_sc_ = vbr_scale;
+  vbr_rs_ = 1.0f / vbr_scale;
+  planned(B, st, [&] {
+    View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
+    View y = g_a(xv);
+    View z = h_a(y);
+    View zh = alloc(z.C, z.H, z.W);
+    eb(z, zh, z_lik, nullptr);
+    View hyper = h_s(zh);
+    View yhat = alloc(cfg_.M, y.H, y.W);
+    slice_loop(Mode::Forward, hyper, &y, yhat, y_lik, nullptr, nullptr, nullptr);
+    if (x_hat) {
+      View out{x_hat, 3, H, W, (int64_t)3 * H * W};
+      g_s(yhat, out);
+    }
+  });
+}
+
+void Model::compress(const float* x, int B, int H, int W, float vbr_scale, hipStream_t st) {
+  MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64");
+  MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
+  vbr_on_ = cfg_.vbr;
+  vbr_sc_ = vbr_scale;
+  vbr_rs_ = 1.0f / vbr_scale;
+  const int h = H / 16, w = W / 16, hz = H / 64, wz = W / 64;
+  const int64_t n_per = (int64_t)cfg_.C * h * (w / 2);
+  const int nph = 2 * cfg_.S;
+  const int64_t ny = (int64_t)nph * B * n_per, nz = (int64_t)B * cfg_.N * hz * wz;
+  int32_t *d_sym = nullptr, *d_idx = nullptr, *d_zsym = nullptr;
+  planned(B, st, [&] {
+    d_sym = reinterpret_cast<int32_t*>(arena_.alloc(ny));
+    d_idx = reinterpret_cast<int32_t*>(arena_.alloc(ny));
+    d_zsym = reinterpret_cast<int32_t*>(arena_.alloc(nz));
+    View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
+    View y = g_a(xv);
+    View z = h_a(y);
+    View zh = alloc(z.C, z.H, z.W);
+    eb(z, zh, nullptr, d_zsym);  // z_hat = round(z - med) + med == decompress(compress(z))
+    View hyper = h_s(zh);
+    View yhat = alloc(cfg_.M, y.H, y.W);
+    slice_loop(Mode::Encode, hyper, &y, yhat, nullptr, d_sym, d_idx, nullptr);
+  });
+  ensure_host((size_t)(2 * ny + nz));
+  int32_t* hs = h_sym_;
+  int32_t* hi = h_idx_;
+  int32_t* hz_ = h_sym_ + ny;
+  HIP_OK(hipMemcpyAsync(hs, d_sym, ny * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(hi, d_idx, ny * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(hz_, d_zsym, nz * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  enc_.assign(B, EncodedImage{});
+  const int64_t zper = (int64_t)cfg_.N * hz * wz;
+  auto work = [&](int b) {
+    // y: phases in order, this image's part of each ([phase][B][n_per] on device)
+    std::vector<int32_t> s((size_t)nph * n_per), ix((size_t)nph * n_per);
+    for (int k = 0; k < nph; ++k) {
+      std::memcpy(s.data() + k * n_per, hs + ((int64_t)k * B + b) * n_per, n_per * 4);
+      std::memcpy(ix.data() + k * n_per, hi + ((int64_t)k * B + b) * n_per, n_per * 4);
+    }
+    enc_[b].y = rans_encode(s.data(), ix.data(), (int64_t)s.size(), gc_);
+    enc_[b].y_sym = std::move(s);
+    enc_[b].y_idx = std::move(ix);
+    enc_[b].z_sym.assign(hz_ + b * zper, hz_ + (b + 1) * zper);
+    // z: EntropyBottleneck._build_indexes -> channel index, C-order over [C, hz, wz]
+    std::vector<int32_t> zi(zper);
+    for (int64_t i = 0; i < zper; ++i) zi[i] = (int32_t)(i / ((int64_t)hz * wz));
+    enc_[b].z = rans_encode(hz_ + b * zper, zi.data(), zper, eb_);
+  };
+  if (B == 1) work(0);
+  else {
+    std::vector<std::thread> th;
+    for (int b = 0; b < B; ++b) th.emplace_back(work, b);
+    for (auto& t : th) t.join();
+  }
+}
+
+void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
+                       int B, int hz, int wz, float* x_hat, float vbr_scale, hipStream_t st) {
+  MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
+  vbr_on_ = cfg_.vbr;
+  vbr_sc_ = vbr_scale;
+  vbr_rs_ = 1.0f / vbr_scale;
+  const int h = hz * 4, w = wz * 4;
+  const int64_t n_per = (int64_t)cfg_.C * h * (w / 2);
+  const int64_t zper = (int64_t)cfg_.N * hz * wz;
+  ensure_host((size_t)std::max<int64_t>(B * n_per, B * zper));
+  // z first (host decode, before the network needs it)
+  {
+    std::vector<int32_t> zi(zper);
+    for (int64_t i = 0; i < zper; ++i) zi[i] = (int32_t)(i / ((int64_t)hz * wz));
+    for (int b = 0; b < B; ++b) {
+      RansDecoderState d;
+      d.set_stream(z[b], zlen[b]);
+      d.decode(zi.data(), zper, eb_, h_sym_ + b * zper);
+    }
+  }
+  PhaseDecoder dec(B, y, ylen, &gc_, h_sym_, h_idx_);
+  const int32_t* hz_sym = h_sym_;
+  planned(B, st, [&] {
+    int32_t* d_zsym = reinterpret_cast<int32_t*>(arena_.alloc(B * zper));
+    int32_t* d_sym = reinterpret_cast<int32_t*>(arena_.alloc(B * n_per));
+    int32_t* d_idx = reinterpret_cast<int32_t*>(arena_.alloc(B * n_per));
+    View zh = alloc(cfg_.N, hz, wz);
+    if (!dry_) {
+      HIP_OK(hipMemcpyAsync(d_zsym, hz_sym, B * zper * 4, hipMemcpyHostToDevice, st_));
+      eb_dequant(d_zsym, rw("entropy_bottleneck.quantiles"), zh.p, cfg_.N, hz * wz, B_, st_);
+      HIP_OK(hipStreamSynchronize(st_));  // h_sym_ is reused by the phase decoder
+    }
+    View hyper = h_s(zh);
+    View yhat = alloc(cfg_.M, h, w);
+    slice_loop(Mode::Decode, hyper, nullptr, yhat, nullptr, d_sym, d_idx, &dec);
+    View out{x_hat, 3, 16 * h, 16 * w, (int64_t)3 * 16 * h * 16 * w};
+    g_s(yhat, out);
+  });
+}
+
+// module-level entry points (tests): which in {local, chan, inter, intra, epa, epn, lrpa, lrpn, g_a, h_a, h_s, g_s, rbu}
+void Model::run_module(const std::string& which, int i, const float* in0, const float* in1, int B, int Cin, int H,
+                       int W, float* out, hipStream_t st) {
+  planned(B, st, [&] {
+    View a{const_cast<float*>(in0), Cin, H, W, (int64_t)Cin * H * W};
+    View r;
+    if (which == "local") r = local_context(a, i);
+    else if (which == "chan") r = channel_context(a, i);
+    else if (which == "inter") r = inter_context(a, i);
+    else if (which == "intra") {
+      View b{const_cast<float*>(in1), Cin, H, W, (int64_t)Cin * H * W};
+      r = intra_context(a, b, i);
+    } else if (which == "epa") r = entropy_parameters({a}, "anchor", i);
+    else if (which == "epn") r = entropy_parameters({a}, "nonanchor", i);
+    else if (which == "g_a") r = g_a(a);
+    else if (which == "h_a") r = h_a(a);
+    else if (which == "h_s") r = h_s(a);
+    else if (which == "rbu") r = rbu(a, "g_s.synthesis_transform." + std::to_string(i));
+    else if (which == "rbws") r = rbws(a, "g_a.analysis_transform." + std::to_string(i), !cfg_.sd);
+    else if (which == "g_s") {
+      View o{out, 3, 16 * H, 16 * W, (int64_t)3 * 256 * H * W};
+      g_s(a, o);
+      return;
+    } else if (which == "lrpn") {
+      // in0 = LRP input, in1 = residual slice (copied to out first); out = res + mask(0.5 tanh(lrp(x)))
+      View o{out, cfg_.C, H, W, (int64_t)cfg_.C * H * W};
+      if (!dry_) HIP_OK(hipMemcpyAsync(out, in1, sizeof(float) * B * o.bs, hipMemcpyDeviceToDevice, st_));
+      lrp({a}, "nonanchor", i, o, false);
+      return;
+    } else throw Error("mlic: unknown module " + which);
+    if (!dry_) HIP_OK(hipMemcpyAsync(out, r.p, sizeof(float) * B * r.bs, hipMemcpyDeviceToDevice, st_));
+  });
+}
+
+}  // namespace mlic

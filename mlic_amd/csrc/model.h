@@ -1,0 +1,147 @@
+// MLIC++ model executor: the reference's module graph (models/mlicpp.py, mlicpp_small_decoder.py,
+// mlicpp_vbr.py) driven natively over the HIP kernels, on one stream, with a per-handle arena.
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+#include "rans.h"
+
+namespace mlic {
+
+struct Cfg {
+  std::string name;
+  int N = 0, M = 0, S = 0, C = 0, win = 5;
+  bool sd = false, vbr = false;
+  int hM() const { return sd ? M / 4 : M; }
+  int gN() const { return sd ? N / 4 : N; }
+};
+Cfg config_for(const std::string& name);
+
+struct ConvW {
+  float* w = nullptr;        // packed [K*K][Cin][Cout]
+  const float* b = nullptr;  // [Cout] or null
+  int Cin = 0, Cout = 0, K = 0;
+};
+struct DwW {
+  const float* w = nullptr;  // [C][9]
+  const float* b = nullptr;
+  int C = 0;
+};
+
+// arena: stream-ordered bump allocator; a dry run sizes it
+class Arena {
+ public:
+  ~Arena();
+  void ensure(size_t bytes);
+  float* alloc(int64_t nfloats);
+  size_t mark() const { return top_; }
+  void release(size_t m) { top_ = m; }
+  void begin(bool dry) { dry_ = dry; top_ = 0; peak_ = 0; }
+  size_t peak() const { return peak_; }
+  size_t capacity() const { return cap_; }
+
+ private:
+  char* base_ = nullptr;
+  size_t cap_ = 0, top_ = 0, peak_ = 0;
+  bool dry_ = false;
+};
+
+struct EncodedImage {
+  std::string y;  // one rANS stream for all slices/phases
+  std::string z;  // z stream (EntropyBottleneck)
+  std::vector<int32_t> y_sym, y_idx, z_sym;  // the coder inputs, in coder order (tests / tooling)
+};
+
+class Model {
+ public:
+  Model(const std::string& name, int n, const char* const* names, const float* const* ptrs, const int64_t* shapes,
+        const int* ndims, hipStream_t st);
+  ~Model();
+  const Cfg& cfg() const { return cfg_; }
+
+  // forward(): x [B,3,H,W] -> x_hat, y_lik [B,M,H/16,W/16], z_lik [B,N,H/64,W/64] (any may be null)
+  void forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
+               hipStream_t st);
+  // compress(): network + rANS; results readable with encoded(b)
+  void compress(const float* x, int B, int H, int W, float vbr_scale, hipStream_t st);
+  const EncodedImage& encoded(int b) const { return enc_.at(b); }
+  // decompress(): y/z byte streams per image -> x_hat [B,3,4*16*hz,4*16*wz]
+  void decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen, int B,
+                  int hz, int wz, float* x_hat, float vbr_scale, hipStream_t st);
+  void set_tables(const CdfTables& gc, const CdfTables& eb) {
+    gc_ = gc;
+    eb_ = eb;
+  }
+  size_t arena_bytes() const { return arena_.capacity(); }
+  size_t weight_bytes() const { return wbytes_; }
+  // module-level entry points for tests
+  void run_module(const std::string& which, int idx, const float* in0, const float* in1, int B, int Cin, int H, int W,
+                  float* out, hipStream_t st);
+
+ private:
+  enum class Mode { Forward, Encode, Decode };
+  Cfg cfg_;
+  std::map<std::string, ConvW> convs_;
+  std::map<std::string, DwW> dws_;
+  std::map<std::string, const float*> raw_;
+  std::vector<void*> owned_;
+  size_t wbytes_ = 0;
+  float* scale_table_ = nullptr;
+  int* rel_index_ = nullptr;
+  Arena arena_;
+  // per-call state
+  hipStream_t st_ = nullptr;
+  int B_ = 0;
+  bool dry_ = false;
+  float vbr_sc_ = 1.0f, vbr_rs_ = 1.0f;
+  bool vbr_on_ = false;
+  CdfTables gc_, eb_;
+  std::vector<EncodedImage> enc_;
+  // host staging for the coder
+  int32_t* h_sym_ = nullptr;
+  int32_t* h_idx_ = nullptr;
+  size_t h_cap_ = 0;
+
+  // -- weights
+  const ConvW& cw(const std::string& k) const;
+  const DwW& dww(const std::string& k) const;
+  const float* rw(const std::string& k) const;
+  bool has(const std::string& k) const { return convs_.count(k) || dws_.count(k) || raw_.count(k); }
+
+  // -- building blocks (outputs allocated in the arena unless given)
+  View alloc(int C, int H, int W);
+  void conv(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
+            const View* aux = nullptr, const View* res = nullptr);
+  void dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu);
+  View conv3x3(const std::vector<View>& ins, const std::string& p, int stride, bool dwsep, int epi,
+               const View* res = nullptr, const View* out = nullptr);
+  View conv1x1(const View& in, const std::string& p, int stride, int epi, const View* res = nullptr);
+  void gdn(const View& x, const std::string& p, bool inverse, const View& out, const View* res);
+  View rbws(const View& x, const std::string& p, bool dwsep);
+  View rb(const View& x, const std::string& p, bool dwsep);
+  View rbu(const View& x, const std::string& p);
+  View g_a(const View& x);
+  View h_a(const View& y);
+  View h_s(const View& z_hat);
+  void g_s(const View& y_hat, const View& out);
+  View local_context(const View& x, int i);
+  View channel_context(const View& x, int i);
+  View inter_context(const View& x, int i);
+  View intra_context(const View& x1, const View& x2, int i);
+  View entropy_parameters(const std::vector<View>& ins, const std::string& kind, int i);
+  void lrp(const std::vector<View>& ins, const std::string& kind, int i, const View& yh_slice, bool anchor);
+  View qkv_branch(const View& x, const std::string& p);
+  void slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, int32_t* d_sym,
+                  int32_t* d_idx, class PhaseDecoder* dec);
+  void eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym);
+
+  template <class F>
+  void planned(int B, hipStream_t st, F&& body);
+  void ensure_host(size_t n);
+};
+
+}  // namespace mlic

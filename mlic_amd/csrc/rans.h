@@ -1,0 +1,39 @@
+// Host-native rANS entropy coder, byte-compatible with compressai 1.2.6's
+// BufferedRansEncoder / RansDecoder (ryg_rans 64-bit state, 32-bit words, 16-bit CDF
+// precision, 4-bit bypass escapes for out-of-range values), and pmf_to_quantized_cdf.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mlic {
+
+struct CdfTables {
+  // table k: cdf[k * stride .. + length[k]]  (length includes the two sentinels, as compressai)
+  std::vector<int32_t> cdf;
+  std::vector<int32_t> length;
+  std::vector<int32_t> offset;
+  int stride = 0;
+  int n = 0;
+  bool empty() const { return n == 0; }
+};
+
+// Encodes symbols[i] with table indexes[i]; returns the byte string (little-endian u32 words).
+std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t);
+
+class RansDecoderState {
+ public:
+  void set_stream(const uint8_t* data, size_t nbytes);
+  // decodes n symbols with the given table indexes
+  void decode(const int32_t* indexes, int64_t n, const CdfTables& t, int32_t* out);
+
+ private:
+  std::vector<uint32_t> words_;
+  size_t pos_ = 0;
+  uint64_t state_ = 0;
+  uint32_t get_word();
+};
+
+std::vector<uint32_t> pmf_to_quantized_cdf(const float* pmf, int n, int precision);
+
+}  // namespace mlic

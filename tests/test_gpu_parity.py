@@ -1,0 +1,187 @@
+"""HIP path vs the reference fixtures and the CPU oracle (needs a MI355X: `-m gpu`).
+
+Tolerances (BASELINE.json north_star): bpp within 1e-3, PSNR within 0.01 dB of the reference CPU
+path; checkerboard / mask / slice bookkeeping bit-exact; tensors to fp32 summation-order noise.
+"""
+import hashlib
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import mlic_ref_cpu as ref
+from mlic_amd import entropy, get_model, synthetic
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+_NETS = {}
+
+
+def net_for(name, seed=0):
+    key = (name, seed)
+    if key not in _NETS:
+        n = get_model(name)
+        n.load_state_dict(synthetic.synth_state_dict(name, seed))
+        _NETS[key] = n.to(DEV).eval()
+    return _NETS[key]
+
+
+def bpp(out, npix):
+    return ref.bpp_from_likelihoods(out["likelihoods"]["y_likelihoods"].cpu().double().float(),
+                                    out["likelihoods"]["z_likelihoods"].cpu(), npix)
+
+
+def maxdiff(a, b):
+    return (torch.as_tensor(np.asarray(a)).float() - torch.as_tensor(np.asarray(b)).float()).abs().max().item()
+
+
+def test_local_attn_mask_bitexact(golden):
+    g = golden("masks.npz")
+    from mlic_amd import _lib
+    import ctypes as C
+    for k in g.files:
+        if not k.startswith("mask_"):
+            continue
+        H, W = map(int, k[5:].split("x"))
+        out = torch.empty(H * W, 25, 25, device=DEV)
+        _lib.call("mlic_local_attn_mask", C.c_void_p(torch.cuda.current_stream().cuda_stream), out.data_ptr(), H, W)
+        assert torch.equal(out.cpu(), torch.from_numpy(g[k])), k
+
+
+def test_module_vectors(golden):
+    g = golden("modules_L.npz")
+    net = net_for("MLICPP_L")
+    T = lambda k: torch.from_numpy(g[k]).to(DEV)
+    cases = [
+        ("local", 0, "lc_in", None, "lc_out", 1e-4),
+        ("chan", 3, "chan3_in", None, "chan3_out", 1e-4),
+        ("inter", 3, "chan3_in", None, "inter3_out", 1e-4),
+        ("inter", 9, "inter9_in", None, "inter9_out", 2e-4),
+        ("intra", 1, "intra_in1", "intra_in2", "intra_out", 1e-4),
+        ("epa", 2, "epa2_in", None, "epa2_out", 1e-4),
+        ("rbu", 1, "rbu1_in", None, "rbu1_out", 2e-4),
+        ("rbws", 0, "rbws0_in", None, "rbws0_out", 1e-4),
+    ]
+    for which, idx, a, b, o, tol in cases:
+        exp = g[o]
+        got = net.run_module(which, idx, T(a), None if b is None else T(b), out_shape=exp.shape)
+        torch.cuda.synchronize()
+        scale = max(1.0, float(np.abs(exp).max()))
+        assert maxdiff(got.cpu(), exp) <= tol * scale, (which, idx, maxdiff(got.cpu(), exp))
+    # LRP non-anchor with its masked residual epilogue
+    res = torch.randn(1, 32, 8, 12, generator=torch.Generator().manual_seed(5)).to(DEV)
+    got = net.run_module("lrpn", 2, T("lrpn2_in"), res, out_shape=(1, 32, 8, 12)).cpu()
+    exp = res.cpu() + ref.ckbd_nonanchor(torch.from_numpy(g["lrpn2_out"]))
+    assert maxdiff(got, exp) <= 1e-5
+
+
+FWD = [("MLICPP_L", 128, 192, None), ("MLICPP_L", 128, 128, None), ("MLICPP_S", 128, 128, None),
+       ("MLICPP_S2", 128, 128, None), ("MLICPP_M", 128, 128, None), ("MLICPP_M_SMALL_DEC", 128, 128, None),
+       ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5)]
+
+
+@pytest.mark.parametrize("name,H,W,s", FWD)
+def test_forward_matches_reference_fixture(golden, name, H, W, s):
+    tag = f"{name}_{H}x{W}" + ("" if s is None else f"_s{s}")
+    g = golden(f"forward_{tag}.npz")
+    img_seed = 1 if (name == "MLICPP_L" and W == 128) else 0
+    x = synthetic.synth_image(H, W, img_seed)
+    net = net_for(name)
+    out = net(x.to(DEV)) if s is None else net(x.to(DEV), stage=2, s=s)
+    torch.cuda.synchronize()
+    b = bpp(out, H * W)
+    assert abs(b - float(g["bpp"])) <= 1e-3, (b, float(g["bpp"]))
+    p_ref = ref.psnr_uint8(x, torch.from_numpy(g["x_hat"]))
+    p_gpu = ref.psnr_uint8(x, out["x_hat"].cpu())
+    assert abs(p_gpu - p_ref) <= 0.01, (p_gpu, p_ref)
+    assert maxdiff(out["x_hat"].cpu(), g["x_hat"]) <= 2e-3
+    assert maxdiff(out["likelihoods"]["z_likelihoods"].cpu(), g["z_lik"]) <= 1e-4
+
+
+@pytest.mark.parametrize("name,B,H,W", [("MLICPP_L", 2, 192, 128), ("MLICPP_S2", 1, 128, 256),
+                                        ("MLICPP_M_SMALL_DEC", 2, 128, 192)])
+def test_forward_matches_oracle_batched(name, B, H, W):
+    xs = torch.cat([synthetic.synth_image(H, W, 10 + i) for i in range(B)])
+    sd = synthetic.synth_state_dict(name, 0)
+    o = ref.RefMLIC(name, sd).forward(xs)
+    out = net_for(name)(xs.to(DEV))
+    torch.cuda.synchronize()
+    for i in range(B):
+        bg = ref.bpp_from_likelihoods(out["likelihoods"]["y_likelihoods"][i:i + 1].cpu(),
+                                      out["likelihoods"]["z_likelihoods"][i:i + 1].cpu(), H * W)
+        bc = ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"][i:i + 1],
+                                      o["likelihoods"]["z_likelihoods"][i:i + 1], H * W)
+        assert abs(bg - bc) <= 1e-3
+        assert abs(ref.psnr_uint8(xs[i:i + 1], out["x_hat"][i:i + 1].cpu())
+                   - ref.psnr_uint8(xs[i:i + 1], o["x_hat"][i:i + 1])) <= 0.01
+    assert maxdiff(out["x_hat"].cpu(), o["x_hat"]) <= 2e-3
+
+
+@pytest.mark.parametrize("name,H,W", [("MLICPP_L", 128, 192), ("MLICPP_S", 128, 128),
+                                      ("MLICPP_M_SMALL_DEC", 128, 128)])
+def test_compress_streams_match_reference(golden, name, H, W):
+    """Coder inputs vs the exact symbol/index lists the reference hands to its rANS encoder.
+    fp32 summation order may flip a rounding decision, so allow a tiny mismatch fraction."""
+    g = golden(f"forward_{name}_{H}x{W}.npz")
+    net = net_for(name)
+    net.update()
+    x = synthetic.synth_image(H, W, 0).to(DEV)
+    c = net.compress(x)
+    ys, yi, zs = net.encoded_streams(0)
+    assert ys.shape == g["y_symbols"].shape
+    assert np.mean(ys != g["y_symbols"]) <= 1e-3
+    assert np.mean(yi != g["y_indexes"]) <= 1e-3
+    assert np.array_equal(zs, g["z_symbols"].reshape(-1))
+    # the bytes decode back to exactly what was coded
+    gc = net.gaussian_conditional
+    dec = entropy.rans_decode(c["strings"][0][0], yi, gc._quantized_cdf.cpu(), gc._cdf_length.cpu(),
+                              gc._offset.cpu())
+    assert np.array_equal(dec, ys)
+
+
+@pytest.mark.parametrize("name,B,H,W,s", [("MLICPP_L", 1, 128, 192, None), ("MLICPP_L", 2, 128, 128, None),
+                                          ("MLICPP_S", 1, 192, 128, None), ("MLICPP_M_SMALL_DEC", 1, 128, 128, None),
+                                          ("MLICPP_L_VBR", 1, 128, 128, 2)])
+def test_roundtrip_bitexact(name, B, H, W, s):
+    """decompress(compress(x)).x_hat == forward(x).x_hat, bit for bit (same kernels, same ŷ)."""
+    net = net_for(name)
+    net.update()
+    x = torch.cat([synthetic.synth_image(H, W, 20 + i) for i in range(B)]).to(DEV)
+    kw = {} if s is None else {"stage": 2, "s": s}
+    f = net(x, **kw)
+    c = net.compress(x, **kw)
+    d = net.decompress(c["strings"], c["shape"], **kw)
+    assert torch.equal(d["x_hat"], f["x_hat"])
+
+
+def test_1080p_parity_and_roundtrip():
+    """BASELINE config 2 size: 1920x1088 MLICPP_L, bpp / PSNR vs the CPU oracle, and the
+    size-independent round-trip invariant at full size."""
+    name, H, W = "MLICPP_L", 1088, 1920
+    x = synthetic.synth_image(H, W, 0)
+    net = net_for(name)
+    out = net(x.to(DEV))
+    torch.cuda.synchronize()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    o = ref.RefMLIC(name, synthetic.synth_state_dict(name, 0)).forward(x)
+    bg, bc = bpp(out, H * W), ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"],
+                                                      o["likelihoods"]["z_likelihoods"], H * W)
+    pg, pc = ref.psnr_uint8(x, out["x_hat"].cpu()), ref.psnr_uint8(x, o["x_hat"])
+    assert abs(bg - bc) <= 1e-3, (bg, bc)
+    assert abs(pg - pc) <= 0.01, (pg, pc)
+    net.update()
+    c = net.compress(x.to(DEV))
+    d = net.decompress(c["strings"], c["shape"])
+    assert torch.equal(d["x_hat"], out["x_hat"])
+    nbytes = len(c["strings"][0][0]) + len(c["strings"][1][0])
+    # file bpp tracks the likelihood bpp (coder overhead small)
+    assert abs(8 * nbytes / (H * W) - bg) / bg < 0.02
+
+
+def test_cpu_tensor_raises():
+    net = net_for("MLICPP_S")
+    with pytest.raises(RuntimeError):
+        net.cpu()(torch.zeros(1, 3, 64, 64))
+    net.to(DEV)
