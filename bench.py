@@ -1,0 +1,210 @@
+"""MLIC++ encode+decode throughput on MI355X (BASELINE.json config 2).
+
+One step = compress() + decompress() of a batch of synthetic 1920x1088 images on each GPU with
+MLICPP_L (seeded conditioned weights; no checkpoints offline).  Images shard across ranks (one
+process per GPU, weak scaling); the only collective is an all_gather of fixed-size per-image
+records (bpp/PSNR/bytes) after the timed region — SURVEY §8(e).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel family (the MFMA implicit-GEMM
+conv, ~95 % of the FLOPs) measured live with HIP events on the executor's stream in an extra,
+untimed step; `cpu_baseline` times the CPU oracle (torch fp32, this box's cores) on one image.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec (enc+dec) at 1920×1088 MLICPP_L, 1/2/4/8 GPU; bpp/PSNR Δ vs ref"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense, exact f32)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=4, help="images per GPU per step")
+    ap.add_argument("--model", default="MLICPP_L")
+    ap.add_argument("--height", type=int, default=1088)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                    help="PMC-derived HBM bytes per conv launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def psnr_u8(a: torch.Tensor, b: torch.Tensor) -> float:
+    """utils/utils.py:86-87 (clamp, *255, truncate) + utils/metrics.py:32-33."""
+    qa = (a.clamp(0, 1) * 255).to(torch.uint8).float()
+    qb = (b.clamp(0, 1) * 255).to(torch.uint8).float()
+    mse = torch.mean((qa - qb) ** 2).item()
+    return 20 * math.log10(255.0) - 10 * math.log10(mse) if mse > 0 else float("inf")
+
+
+def cpu_baseline(model: str, H: int, W: int):
+    """Oracle (torch CPU fp32 restatement of the reference) enc+dec of one image, with the native
+    rANS coder for the entropy-coding part; threads = this process's CPU affinity (<= 32)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mlic_ref_cpu as ref
+    from mlic_amd import entropy, synthetic
+    cores = max(1, min(32, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(cores)
+    sd = synthetic.synth_state_dict(model, 0)
+    m = ref.RefMLIC(model, sd)
+    x = synthetic.synth_image(H, W, 0)
+    tables = entropy.gaussian_tables(entropy.get_scale_table())
+    t0 = time.time()
+    st = m.compress_streams(x)
+    sym = torch.cat([p[0].reshape(-1) for p in st["phases"]]).numpy()
+    idx = torch.cat([p[1].reshape(-1) for p in st["phases"]]).numpy()
+    data = entropy.rans_encode(sym, idx, *tables[:3])
+    dec = entropy.rans_decode(data, idx, *tables[:3])
+    # decoder network: phases fed from the decoded symbols
+    offs = np.cumsum([0] + [p[0].numel() for p in st["phases"]])
+    phase_syms = [torch.from_numpy(dec[offs[k]:offs[k + 1]]).reshape(st["phases"][k][0].shape)
+                  for k in range(len(st["phases"]))]
+    m.decode_streams(st["z_symbols"], phase_syms)
+    dt = time.time() - t0
+    return {"value": round(1.0 / dt, 5), "unit": "images/sec (enc+dec)", "cores": cores, "kind": "port",
+            "sample": f"1 image {W}x{H} {model}: oracle torch-CPU fp32 encoder+decoder networks + native rANS, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from mlic_amd import _lib, get_model, synthetic
+    net = get_model(a.model)
+    net.load_state_dict(synthetic.synth_state_dict(a.model, 0))
+    net = net.to(dev).eval()
+    net.update()
+    B, H, W = a.batch, a.height, a.width
+    x = torch.cat([synthetic.synth_image(H, W, 1000 * rank + i) for i in range(B)]).to(dev)
+
+    def step():
+        c = net.compress(x)
+        d = net.decompress(c["strings"], c["shape"])
+        return c, d
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        c, d = step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # per-image records {bytes, bpp_file, psnr}: the one collective (all_gather, RCCL over xGMI)
+    rec = torch.zeros(B, 3, dtype=torch.float64, device=dev)
+    for i in range(B):
+        nbytes = len(c["strings"][0][i]) + len(c["strings"][1][i])
+        rec[i, 0] = nbytes
+        rec[i, 1] = 8.0 * nbytes / (H * W)
+        rec[i, 2] = psnr_u8(x[i], d["x_hat"][i])
+    if distributed:
+        allrec = [torch.zeros_like(rec) for _ in range(world)]
+        dist.all_gather(allrec, rec)
+        rec = torch.cat(allrec)
+    rec = rec.cpu()
+
+    # live roofline of the dominant kernel family: one extra profiled (untimed) step
+    h = net._handle
+    _lib.call("mlic_set_profiling", h, 1)
+    step()
+    torch.cuda.synchronize()
+    _lib.call("mlic_set_profiling", h, 0)
+    fam = {}
+    for cat, nm in enumerate(["conv_mfma", "dw3x3", "local_attn", "linear_attn", "elementwise"]):
+        n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
+        _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
+        fam[nm] = {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
+    conv = fam["conv_mfma"]
+    achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12 if conv["ms"] > 0 else 0.0
+    traffic = None
+    try:
+        with open(a.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("model") == a.model and tj.get("H") == H and tj.get("W") == W:
+            traffic = tj.get("conv_hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    step_gpu_ms = sum(v["ms"] for v in fam.values())
+
+    if rank == 0:
+        images = B * world * a.steps
+        out = {
+            "metric": METRIC,
+            "value": round(images / elapsed, 4),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded sinusoid images, seeded conditioned weights)",
+            "config": {"workload": f"{a.model} compress+decompress (full rANS bitstreams) of {W}x{H} images",
+                       "model": a.model, "global_batch": B * world, "per_gpu_batch": B, "H": H, "W": W,
+                       "parallelism": f"image-sharded x{world} (no cross-GPU context)"},
+            "roofline": {"bound": "mfma", "kernel": "conv_mfma (implicit-GEMM conv, v_mfma_f32_32x32x2_f32)",
+                         "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                         "traffic": traffic,
+                         "launches_per_step": conv["launches"],
+                         "avg_launch_us": round(1000 * conv["ms"] / max(1, conv["launches"]), 2),
+                         "algorithmic_flops_per_launch": round(conv["flops"] / max(1, conv["launches"]))},
+            "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items()},
+            "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
+            "quality": {"bpp_file_mean": round(float(rec[:, 1].mean()), 5),
+                        "psnr_u8_mean": round(float(rec[:, 2].mean()), 4), "images": int(rec.shape[0])},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a.model, H, W)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -63,6 +63,11 @@ int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, con
                     int B, int Cin, int H, int W, float* out);
 int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
 
+/* live kernel timing (HIP events on the executor stream): categories 0 conv_mfma, 1 depthwise,
+ * 2 local attention, 3 linear attention, 4 elementwise/reductions.  read() sums and clears. */
+int mlic_set_profiling(mlic_model* m, int on);
+int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes);
+
 /* kernel-level entry points (bit-exact tests) */
 int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */
 int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);

@@ -141,6 +141,21 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
   });
 }
 
+int mlic_set_profiling(mlic_model* m, int on) {
+  return guard([&] { m->impl->set_profiling(on != 0); });
+}
+
+int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes) {
+  return guard([&] {
+    MLIC_CHECK(cat >= 0 && cat < PROF_NCAT, "profile category");
+    ProfStat s = m->impl->profile_read(cat);
+    *launches = s.launches;
+    *ms = s.ms;
+    *flops = s.flops;
+    *bytes = s.bytes;
+  });
+}
+
 int mlic_local_attn_mask(void* stream, float* out, int H, int W) {
   return guard([&] { local_mask(out, H, W, (hipStream_t)stream); });
 }

@@ -238,7 +238,10 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
     P.epi |= EPI_RES;
   }
   P.B = B_;
-  if (!dry_) conv_forward(P, st_);
+  const double outn = (double)B_ * w.Cout * P.Ho * P.Wo;
+  const double flops = 2.0 * outn * cin * w.K * w.K;
+  const double bytes = 4.0 * ((double)B_ * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
+  timed(PROF_CONV, flops, bytes, [&] { conv_forward(P, st_); });
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {
@@ -263,7 +266,8 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
   P.out_bs = out.bs;
   P.gelu = gelu ? 1 : 0;
   P.B = B_;
-  if (!dry_) dw3x3(P, st_);
+  const double outn = (double)B_ * c * P.Ho * P.Wo;
+  timed(PROF_DW, 18.0 * outn, 4.0 * ((double)B_ * c * P.H * P.W + outn), [&] { dw3x3(P, st_); });
 }
 
 // conv3x3 of the fork (modules/layers/conv.py:22-32): DepthWiseConv (dw 3x3 -> pw 1x1) by default,
@@ -423,10 +427,13 @@ View Model::local_context(const View& x, int i) {
   View out = alloc(2 * C, H, W);
   const size_t m = arena_.mark();
   View n1 = alloc(C, H, W);
-  if (!dry_) ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, B_, st_);
+  const double pix = (double)B_ * H * W;
+  timed(PROF_ELEM, 8.0 * pix * C, 8.0 * pix * C, [&] {
+    ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, B_, st_);
+  });
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
   View t = alloc(25 * C, H, W);
-  if (!dry_) {
+  {
     LocalAttnParams A{};
     A.qkv = qkv.p;
     A.qkv_bs = qkv.bs;
@@ -439,13 +446,16 @@ View Model::local_context(const View& x, int i) {
     A.H = H;
     A.W = W;
     A.B = B_;
-    local_attn(A, st_);
+    // per pixel: 2 heads x 25 query cells x 25 keys x hd (QK) + the same for AV
+    const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
+    timed(PROF_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, st_); });
   }
   View f = conv1x1(t, p + ".fusion", 1, EPI_NONE);
   View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
   View n2 = alloc(2 * C, H, W);
-  if (!dry_)
+  timed(PROF_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
     ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, B_, st_);
+  });
   View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
   conv({h1}, cw(p + ".mlp.fc2"), 1, 0, out, EPI_NONE, nullptr, &pj);
   arena_.release(m);
@@ -496,11 +506,11 @@ View Model::inter_context(const View& x, int i) {
   const int nsplit = ctx_splits(HW);
   float* part = arena_.alloc((int64_t)B_ * heads * nsplit * hd * hd);
   float* ctx = arena_.alloc((int64_t)B_ * heads * hd * hd);
-  if (!dry_) {
+  timed(PROF_LINATT, (double)B_ * HW * D * hd * 4.0, 4.0 * B_ * HW * D * 6.0, [&] {
     softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, B_, 0, st_);
     softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, B_, 0, st_);
     linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, B_, nsplit, st_);
-  }
+  });
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
   conv({att}, rp, 1, 2, a, EPI_NONE);
@@ -523,10 +533,10 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   const size_t m = arena_.mark();
   View x1n = alloc(D, H, W);
   View x1a = alloc(D, H, W);
-  if (!dry_) {
+  timed(PROF_ELEM, 0.0, 16.0 * B_ * D * HW, [&] {
     ckbd_mask(x1.p, x1.bs, x1n.p, x1n.bs, D, H, W, B_, 0, st_);
     ckbd_mask(x1.p, x1.bs, x1a.p, x1a.bs, D, H, W, B_, 1, st_);
-  }
+  });
   View q = qkv_branch(x1n, p + ".queries");
   View k = qkv_branch(x1a, p + ".keys");
   View v = qkv_branch(x2, p + ".values");
@@ -536,11 +546,11 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   const int nsplit = ctx_splits(HW);
   float* part = arena_.alloc((int64_t)B_ * heads * nsplit * hd * hd);
   float* ctx = arena_.alloc((int64_t)B_ * heads * hd * hd);
-  if (!dry_) {
+  timed(PROF_LINATT, (double)B_ * HW * D * hd * 4.0, 4.0 * B_ * HW * D * 6.0, [&] {
     softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, B_, 1, st_);
     softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, B_, 2, st_);
     linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, B_, nsplit, st_);
-  }
+  });
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
   conv({att}, rp, 1, 2, a, EPI_NONE);
@@ -689,7 +699,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.sym = d_sym + (int64_t)phase_id * B_ * n_per;
           Q.idx = d_idx + (int64_t)phase_id * B_ * n_per;
         }
-        if (!dry_) quant_phase(Q, st_);
+        timed(PROF_ELEM, 0.0, 4.0 * B_ * C * HW * 5, [&] { quant_phase(Q, st_); });
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
       lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
@@ -699,7 +709,6 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
 }
 
 void Model::eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym) {
-  if (dry_) return;
   EbParams P{};
   const std::string p = "entropy_bottleneck";
   P.z = z.p;
@@ -716,7 +725,7 @@ void Model::eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym) {
   P.H = z.H;
   P.W = z.W;
   P.B = B_;
-  eb_forward(P, st_);
+  timed(PROF_ELEM, 0.0, 12.0 * B_ * z.C * z.H * z.W, [&] { eb_forward(P, st_); });
 }
 
 template <class F>
@@ -740,6 +749,55 @@ void Model::ensure_host(size_t n) {
   HIP_OK(hipHostMalloc(&h_sym_, n * sizeof(int32_t)));
   HIP_OK(hipHostMalloc(&h_idx_, n * sizeof(int32_t)));
   h_cap_ = n;
+}
+
+hipEvent_t Model::next_event() {
+  if (ev_used_ == ev_pool_.size()) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    ev_pool_.push_back(e);
+  }
+  return ev_pool_[ev_used_++];
+}
+
+template <class F>
+void Model::timed(int cat, double flops, double bytes, F&& launch) {
+  if (dry_) return;
+  if (!prof_) {
+    launch();
+    return;
+  }
+  ProfRec r;
+  r.a = next_event();
+  r.b = next_event();
+  r.cat = cat;
+  r.flops = flops;
+  r.bytes = bytes;
+  HIP_OK(hipEventRecord(r.a, st_));
+  launch();
+  HIP_OK(hipEventRecord(r.b, st_));
+  recs_.push_back(r);
+}
+
+ProfStat Model::profile_read(int cat) {
+  ProfStat s;
+  std::vector<ProfRec> keep;
+  for (auto& r : recs_) {
+    if (r.cat != cat) {
+      keep.push_back(r);
+      continue;
+    }
+    HIP_OK(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
+    s.launches += 1;
+    s.ms += ms;
+    s.flops += r.flops;
+    s.bytes += r.bytes;
+  }
+  recs_.swap(keep);
+  if (recs_.empty()) ev_used_ = 0;
+  return s;
 }
 
 // ------------------------------------------------------------------------------------- entry points

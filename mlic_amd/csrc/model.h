@@ -50,6 +50,13 @@ class Arena {
   bool dry_ = false;
 };
 
+// live per-kernel-family timing with HIP events on the executor's stream (bench.py roofline)
+enum ProfCat : int { PROF_CONV = 0, PROF_DW = 1, PROF_LOCAL = 2, PROF_LINATT = 3, PROF_ELEM = 4, PROF_NCAT = 5 };
+struct ProfStat {
+  int64_t launches = 0;
+  double ms = 0, flops = 0, bytes = 0;
+};
+
 struct EncodedImage {
   std::string y;  // one rANS stream for all slices/phases
   std::string z;  // z stream (EntropyBottleneck)
@@ -77,6 +84,8 @@ class Model {
     eb_ = eb;
   }
   size_t arena_bytes() const { return arena_.capacity(); }
+  void set_profiling(bool on) { prof_ = on; }
+  ProfStat profile_read(int cat);  // synchronises the recorded events; clears that category
   size_t weight_bytes() const { return wbytes_; }
   // module-level entry points for tests
   void run_module(const std::string& which, int idx, const float* in0, const float* in1, int B, int Cin, int H, int W,
@@ -101,6 +110,19 @@ class Model {
   bool vbr_on_ = false;
   CdfTables gc_, eb_;
   std::vector<EncodedImage> enc_;
+  // profiling
+  struct ProfRec {
+    hipEvent_t a, b;
+    int cat;
+    double flops, bytes;
+  };
+  bool prof_ = false;
+  std::vector<ProfRec> recs_;
+  std::vector<hipEvent_t> ev_pool_;
+  size_t ev_used_ = 0;
+  hipEvent_t next_event();
+  template <class F>
+  void timed(int cat, double flops, double bytes, F&& launch);
   // host staging for the coder
   int32_t* h_sym_ = nullptr;
   int32_t* h_idx_ = nullptr;
