@@ -63,8 +63,9 @@ int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, con
                     int B, int Cin, int H, int W, float* out);
 int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
 
-/* live kernel timing (HIP events on the executor stream): categories 0 conv_mfma, 1 depthwise,
- * 2 local attention, 3 linear attention, 4 elementwise/reductions.  read() sums and clears. */
+/* live kernel timing (HIP events on the executor stream): categories 0..3 conv_mfma_kernel<64,64>,
+ * <64,128>, <128,64>, <128,128>; 4 depthwise; 5 local attention; 6 linear attention;
+ * 7 elementwise/reductions.  read() sums and clears that category. */
 int mlic_set_profiling(mlic_model* m, int on);
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes);
 

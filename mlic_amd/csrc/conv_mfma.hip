@@ -190,6 +190,12 @@ static void launch_conv(const ConvParams& P, hipStream_t st) {
   HIP_OK(hipGetLastError());
 }
 
+int conv_variant(const ConvParams& P) {
+  const int64_t HWo = (int64_t)P.Ho * P.Wo;
+  if (P.Cout <= 64) return HWo >= 128 * 256 ? 1 : 0;
+  return HWo >= 128 * 512 ? 3 : 2;
+}
+
 void conv_forward(const ConvParams& P, hipStream_t st) {
   MLIC_CHECK(P.nseg >= 1 && P.nseg <= MAXSEG, "segment count");
   int tot = 0;
@@ -204,13 +210,11 @@ void conv_forward(const ConvParams& P, hipStream_t st) {
   MLIC_CHECK(!(P.epi & (EPI_GDN | EPI_IGDN)) || P.aux, "GDN needs aux");
   MLIC_CHECK(!(P.epi & EPI_RES) || P.res, "residual pointer");
   MLIC_CHECK(!(P.epi & EPI_SHUFFLE) || P.Cout % 4 == 0, "pixel shuffle needs Cout % 4 == 0");
-  const int64_t HWo = (int64_t)P.Ho * P.Wo;
-  if (P.Cout <= 64) {
-    if (HWo >= 128 * 256) launch_conv<64, 128>(P, st);
-    else launch_conv<64, 64>(P, st);
-  } else {
-    if (HWo >= 128 * 512) launch_conv<128, 128>(P, st);
-    else launch_conv<128, 64>(P, st);
+  switch (conv_variant(P)) {
+    case 0: launch_conv<64, 64>(P, st); break;
+    case 1: launch_conv<64, 128>(P, st); break;
+    case 2: launch_conv<128, 64>(P, st); break;
+    default: launch_conv<128, 128>(P, st); break;
   }
 }
 

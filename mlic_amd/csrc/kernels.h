@@ -5,6 +5,8 @@
 namespace mlic {
 
 // implicit-GEMM conv on MFMA (conv_mfma.hip)
+// tile instantiation chosen for P: 0 = <64,64>, 1 = <64,128>, 2 = <128,64>, 3 = <128,128>
+int conv_variant(const ConvParams& P);
 void conv_forward(const ConvParams& P, hipStream_t st);
 
 struct DwParams {

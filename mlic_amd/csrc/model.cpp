@@ -241,7 +241,7 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
   const double outn = (double)B_ * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * cin * w.K * w.K;
   const double bytes = 4.0 * ((double)B_ * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  timed(PROF_CONV, flops, bytes, [&] { conv_forward(P, st_); });
+  timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, st_); });
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {

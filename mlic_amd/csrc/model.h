@@ -51,7 +51,8 @@ class Arena {
 };
 
 // live per-kernel-family timing with HIP events on the executor's stream (bench.py roofline)
-enum ProfCat : int { PROF_CONV = 0, PROF_DW = 1, PROF_LOCAL = 2, PROF_LINATT = 3, PROF_ELEM = 4, PROF_NCAT = 5 };
+// categories 0..3 = conv_mfma_kernel tile instantiations (see conv_forward), then the others
+enum ProfCat : int { PROF_CONV = 0, PROF_DW = 4, PROF_LOCAL = 5, PROF_LINATT = 6, PROF_ELEM = 7, PROF_NCAT = 8 };
 struct ProfStat {
   int64_t launches = 0;
   double ms = 0, flops = 0, bytes = 0;
