@@ -46,6 +46,10 @@ int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t*
                             int gc_n, int gc_stride, const int32_t* eb_cdf, const int32_t* eb_len,
                             const int32_t* eb_off, int eb_n, int eb_stride);
 
+/* compress/decompress split a batch over `lanes` host threads, each with its own HIP stream and
+ * workspace, so the host rANS coding of one lane overlaps the kernels of another (default 2, or
+ * $MLIC_LANES).  Results are identical for any lane count. */
+int mlic_set_lanes(mlic_model* m, int lanes);
 int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale);
 int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len);
 int mlic_encoded_copy(mlic_model* m, int b, uint8_t* y, uint8_t* z);

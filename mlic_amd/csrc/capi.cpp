@@ -1,6 +1,7 @@
 // C ABI of libmlic_hip.so (include/mlic_hip.h): status codes, thread-local error text.
 #include "../../include/mlic_hip.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -36,6 +37,7 @@ static CdfTables make_tables(const int32_t* cdf, const int32_t* len, const int32
   t.offset.assign(off, off + n);
   for (int i = 0; i < n; ++i)
     MLIC_CHECK(t.length[i] >= 3 && t.length[i] <= stride, "cdf length out of range");
+  t.prepare();
   return t;
 }
 
@@ -51,6 +53,7 @@ int mlic_create(const char* model_name, int n, const char* const* names, const f
     auto* m = new mlic_model{nullptr};
     try {
       m->impl = new Model(model_name, n, names, ptrs, shapes, ndims, (hipStream_t)stream);
+      if (const char* e = std::getenv("MLIC_LANES")) m->impl->set_lanes(std::atoi(e));
     } catch (...) {
       delete m;
       throw;
@@ -139,6 +142,10 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
     *arena = m->impl->arena_bytes();
     *weights = m->impl->weight_bytes();
   });
+}
+
+int mlic_set_lanes(mlic_model* m, int lanes) {
+  return guard([&] { m->impl->set_lanes(lanes); });
 }
 
 int mlic_set_profiling(mlic_model* m, int on) {

@@ -162,9 +162,44 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
 }
 
 Model::~Model() {
+  lanes_.clear();
   for (void* p : owned_) (void)hipFree(p);
-  if (h_sym_) (void)hipHostFree(h_sym_);
-  if (h_idx_) (void)hipHostFree(h_idx_);
+}
+
+Lane::~Lane() {
+  if (h_sym) (void)hipHostFree(h_sym);
+  if (h_idx) (void)hipHostFree(h_idx);
+  for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+  if (own_stream && st) (void)hipStreamDestroy(st);
+}
+
+thread_local Lane* Model::tl_lane_ = nullptr;
+
+Lane& Model::lane(int i) {
+  while ((int)lanes_.size() <= i) {
+    auto l = std::make_unique<Lane>();
+    HIP_OK(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
+    l->own_stream = true;
+    l->prof = prof_;
+    lanes_.push_back(std::move(l));
+  }
+  return *lanes_[i];
+}
+
+void Model::set_lanes(int n) {
+  MLIC_CHECK(n >= 1 && n <= 16, "lanes must be in [1, 16]");
+  nlanes_ = n;
+}
+
+void Model::set_profiling(bool on) {
+  prof_ = on;
+  for (auto& l : lanes_) l->prof = on;
+}
+
+size_t Model::arena_bytes() const {
+  size_t s = 0;
+  for (auto& l : lanes_) s += l->arena.capacity();
+  return s;
 }
 
 const ConvW& Model::cw(const std::string& k) const {
@@ -186,7 +221,7 @@ const float* Model::rw(const std::string& k) const {
 // ------------------------------------------------------------------------------------- blocks
 View Model::alloc(int C, int H, int W) {
   View v;
-  v.p = arena_.alloc((int64_t)B_ * C * H * W);
+  v.p = L().arena.alloc((int64_t)L().B * C * H * W);
   v.C = C;
   v.H = H;
   v.W = W;
@@ -237,11 +272,11 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
     P.res_bs = res->bs;
     P.epi |= EPI_RES;
   }
-  P.B = B_;
-  const double outn = (double)B_ * w.Cout * P.Ho * P.Wo;
+  P.B = L().B;
+  const double outn = (double)L().B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * cin * w.K * w.K;
-  const double bytes = 4.0 * ((double)B_ * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, st_); });
+  const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
+  timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, L().st); });
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {
@@ -265,9 +300,9 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
   P.out = out.p;
   P.out_bs = out.bs;
   P.gelu = gelu ? 1 : 0;
-  P.B = B_;
-  const double outn = (double)B_ * c * P.Ho * P.Wo;
-  timed(PROF_DW, 18.0 * outn, 4.0 * ((double)B_ * c * P.H * P.W + outn), [&] { dw3x3(P, st_); });
+  P.B = L().B;
+  const double outn = (double)L().B * c * P.Ho * P.Wo;
+  timed(PROF_DW, 18.0 * outn, 4.0 * ((double)L().B * c * P.H * P.W + outn), [&] { dw3x3(P, L().st); });
 }
 
 // conv3x3 of the fork (modules/layers/conv.py:22-32): DepthWiseConv (dw 3x3 -> pw 1x1) by default,
@@ -285,11 +320,11 @@ View Model::conv3x3(const std::vector<View>& ins, const std::string& p, int stri
   const DwW& d = dww(p + ".depth_conv");
   const ConvW& w = cw(p + ".point_conv");
   View out = out_opt ? *out_opt : alloc(w.Cout, Ho, Wo);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View t = alloc(d.C, Ho, Wo);
   dw(ins, d, stride, t, false);
   conv({t}, w, 1, 0, out, epi, nullptr, res);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -310,13 +345,13 @@ View Model::rbws(const View& x, const std::string& p, bool dwsep) {
   const int Ho = (x.H - 1) / 2 + 1, Wo = (x.W - 1) / 2 + 1;
   const ConvW& sk = cw(p + ".skip");
   View out = alloc(sk.Cout, Ho, Wo);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View t1 = conv3x3({x}, p + ".conv1", 2, dwsep, EPI_GELU);
   View t2 = conv3x3({t1}, p + ".conv2", 1, dwsep, EPI_NONE);
   View s = alloc(sk.Cout, Ho, Wo);
   conv({x}, sk, 2, 0, s, EPI_NONE);
   gdn(t2, p + ".gdn", false, out, &s);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -325,7 +360,7 @@ View Model::rb(const View& x, const std::string& p, bool dwsep) {
   const bool has_skip = convs_.count(p + ".skip") > 0;
   const int Cout = dwsep ? cw(p + ".conv2.point_conv").Cout : cw(p + ".conv2").Cout;
   View out = alloc(Cout, x.H, x.W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View t1 = conv3x3({x}, p + ".conv1", 1, dwsep, EPI_GELU);
   View id = x;
   if (has_skip) {
@@ -333,7 +368,7 @@ View Model::rb(const View& x, const std::string& p, bool dwsep) {
     conv({x}, cw(p + ".skip"), 1, 0, id, EPI_NONE);
   }
   conv3x3({t1}, p + ".conv2", 1, dwsep, EPI_GELU, &id, &out);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -343,14 +378,14 @@ View Model::rbu(const View& x, const std::string& p) {
   const ConvW& u = cw(p + ".upsample.0");
   const int C = a.Cout / 4;
   View out = alloc(C, 2 * x.H, 2 * x.W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View ta = alloc(C, 2 * x.H, 2 * x.W);
   conv({x}, a, 1, 1, ta, EPI_GELU | EPI_SHUFFLE);
   View tu = alloc(C, 2 * x.H, 2 * x.W);
   conv({x}, u, 1, 1, tu, EPI_SHUFFLE);
   View tc = conv3x3({ta}, p + ".conv", 1, true, EPI_NONE);
   gdn(tc, p + ".igdn", true, out, &tu);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -360,7 +395,7 @@ View Model::g_a(const View& x) {
   const std::string g = "g_a.analysis_transform";
   const int M = cfg_.M;
   View y = alloc(M, (x.H + 15) / 16, (x.W + 15) / 16);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View a = rbws(x, g + ".0", dwsep);
   View b = rb(a, g + ".1", dwsep);
   View c = rbws(b, g + ".2", dwsep);
@@ -368,7 +403,7 @@ View Model::g_a(const View& x) {
   View e = rbws(d, g + ".4", dwsep);
   View f = rb(e, g + ".5", dwsep);
   conv3x3({f}, g + ".6", 2, dwsep, EPI_NONE, nullptr, &y);
-  arena_.release(m);
+  L().arena.release(m);
   return y;
 }
 
@@ -377,13 +412,13 @@ View Model::h_a(const View& y) {
   const bool dwsep = !cfg_.sd;
   const std::string h = "h_a.reduction";
   View z = alloc(cfg_.N, (y.H + 3) / 4, (y.W + 3) / 4);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View a = conv3x3({y}, h + ".0", 1, dwsep, EPI_GELU);
   View b = conv3x3({a}, h + ".2", 1, dwsep, EPI_GELU);
   View c = conv3x3({b}, h + ".4", 2, dwsep, EPI_GELU);
   View d = conv3x3({c}, h + ".6", 1, dwsep, EPI_GELU);
   conv3x3({d}, h + ".8", 2, dwsep, EPI_NONE, nullptr, &z);
-  arena_.release(m);
+  L().arena.release(m);
   return z;
 }
 
@@ -392,7 +427,7 @@ View Model::h_s(const View& z) {
   const std::string h = "h_s.increase";
   const int hM = cfg_.hM();
   View out = alloc(2 * hM, 4 * z.H, 4 * z.W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View a = conv3x3({z}, h + ".0", 1, true, EPI_GELU);
   View b = alloc(hM, 2 * z.H, 2 * z.W);
   conv({a}, cw(h + ".2.0"), 1, 1, b, EPI_GELU | EPI_SHUFFLE);
@@ -400,14 +435,14 @@ View Model::h_s(const View& z) {
   View d = alloc(hM * 3 / 2, 4 * z.H, 4 * z.W);
   conv({c}, cw(h + ".6.0"), 1, 1, d, EPI_GELU | EPI_SHUFFLE);
   conv3x3({d}, h + ".8", 1, true, EPI_NONE, nullptr, &out);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
 // synthesis.py:56-73
 void Model::g_s(const View& yh, const View& out) {
   const std::string g = "g_s.synthesis_transform";
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View a = rb(yh, g + ".0", true);
   View b = rbu(a, g + ".1");
   View c = rb(b, g + ".2", true);
@@ -416,7 +451,7 @@ void Model::g_s(const View& yh, const View& out) {
   View f = rbu(e, g + ".5");
   View h = rb(f, g + ".6", true);
   conv({h}, cw(g + ".7.0"), 1, 1, out, EPI_SHUFFLE);
-  arena_.release(m);
+  L().arena.release(m);
 }
 
 // ------------------------------------------------------------------------------------- MEM++
@@ -425,11 +460,11 @@ View Model::local_context(const View& x, int i) {
   const std::string p = "local_context." + std::to_string(i);
   const int C = x.C, H = x.H, W = x.W;
   View out = alloc(2 * C, H, W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View n1 = alloc(C, H, W);
-  const double pix = (double)B_ * H * W;
+  const double pix = (double)L().B * H * W;
   timed(PROF_ELEM, 8.0 * pix * C, 8.0 * pix * C, [&] {
-    ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, B_, st_);
+    ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, L().B, L().st);
   });
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
   View t = alloc(25 * C, H, W);
@@ -445,20 +480,20 @@ View Model::local_context(const View& x, int i) {
     A.C = C;
     A.H = H;
     A.W = W;
-    A.B = B_;
+    A.B = L().B;
     // per pixel: 2 heads x 25 query cells x 25 keys x hd (QK) + the same for AV
     const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
-    timed(PROF_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, st_); });
+    timed(PROF_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, L().st); });
   }
   View f = conv1x1(t, p + ".fusion", 1, EPI_NONE);
   View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
   View n2 = alloc(2 * C, H, W);
   timed(PROF_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
-    ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, B_, st_);
+    ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, L().B, L().st);
   });
   View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
   conv({h1}, cw(p + ".mlp.fc2"), 1, 0, out, EPI_NONE, nullptr, &pj);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -468,11 +503,11 @@ View Model::channel_context(const View& x, int i) {
   const bool dwsep = !cfg_.sd;
   const int Cout = dwsep ? cw(p + ".4.point_conv").Cout : cw(p + ".4").Cout;
   View out = alloc(Cout, x.H, x.W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View a = conv3x3({x}, p + ".0", 1, dwsep, EPI_GELU);
   View b = conv3x3({a}, p + ".2", 1, dwsep, EPI_GELU);
   conv3x3({b}, p + ".4", 1, dwsep, EPI_NONE, nullptr, &out);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -480,10 +515,10 @@ View Model::channel_context(const View& x, int i) {
 View Model::qkv_branch(const View& x, const std::string& p) {
   const DwW& d = dww(p + ".1");
   View out = alloc(d.C, x.H, x.W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View t = conv1x1(x, p + ".0", 1, EPI_NONE);
   dw({t}, d, 1, out, false);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -496,7 +531,7 @@ View Model::inter_context(const View& x, int i) {
   const int heads = D / 32, hd = 32;  // num_heads = slice_ch * i // 32 (mlicpp.py:50)
   const ConvW& sk = cw(p + ".skip");
   View out = alloc(sk.Cout, H, W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View q = qkv_branch(x, p + ".queries");
   View k = qkv_branch(x, p + ".keys");
   View v = qkv_branch(x, p + ".values");
@@ -504,12 +539,12 @@ View Model::inter_context(const View& x, int i) {
   View qs = alloc(D, H, W);
   View att = alloc(D, H, W);
   const int nsplit = ctx_splits(HW);
-  float* part = arena_.alloc((int64_t)B_ * heads * nsplit * hd * hd);
-  float* ctx = arena_.alloc((int64_t)B_ * heads * hd * hd);
-  timed(PROF_LINATT, (double)B_ * HW * D * hd * 4.0, 4.0 * B_ * HW * D * 6.0, [&] {
-    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, B_, 0, st_);
-    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, B_, 0, st_);
-    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, B_, nsplit, st_);
+  float* part = L().arena.alloc((int64_t)L().B * heads * nsplit * hd * hd);
+  float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
+  timed(PROF_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
+    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 0, L().st);
+    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 0, L().st);
+    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
   });
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
@@ -519,7 +554,7 @@ View Model::inter_context(const View& x, int i) {
   dw({m1}, dww(p + ".mlp.2"), 1, m2, true);
   View s = conv1x1(a, p + ".skip", 1, EPI_NONE);
   conv({m2}, cw(p + ".mlp.4"), 1, 0, out, EPI_NONE, nullptr, &s);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -530,12 +565,12 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   const int D = x1.C, H = x1.H, W = x1.W, HW = H * W;
   const int heads = 2, hd = D / 2;
   View out = alloc(2 * D, H, W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View x1n = alloc(D, H, W);
   View x1a = alloc(D, H, W);
-  timed(PROF_ELEM, 0.0, 16.0 * B_ * D * HW, [&] {
-    ckbd_mask(x1.p, x1.bs, x1n.p, x1n.bs, D, H, W, B_, 0, st_);
-    ckbd_mask(x1.p, x1.bs, x1a.p, x1a.bs, D, H, W, B_, 1, st_);
+  timed(PROF_ELEM, 0.0, 16.0 * L().B * D * HW, [&] {
+    ckbd_mask(x1.p, x1.bs, x1n.p, x1n.bs, D, H, W, L().B, 0, L().st);
+    ckbd_mask(x1.p, x1.bs, x1a.p, x1a.bs, D, H, W, L().B, 1, L().st);
   });
   View q = qkv_branch(x1n, p + ".queries");
   View k = qkv_branch(x1a, p + ".keys");
@@ -544,12 +579,12 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   View qs = alloc(D, H, W);
   View att = alloc(D, H, W);
   const int nsplit = ctx_splits(HW);
-  float* part = arena_.alloc((int64_t)B_ * heads * nsplit * hd * hd);
-  float* ctx = arena_.alloc((int64_t)B_ * heads * hd * hd);
-  timed(PROF_LINATT, (double)B_ * HW * D * hd * 4.0, 4.0 * B_ * HW * D * 6.0, [&] {
-    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, B_, 1, st_);
-    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, B_, 2, st_);
-    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, B_, nsplit, st_);
+  float* part = L().arena.alloc((int64_t)L().B * heads * nsplit * hd * hd);
+  float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
+  timed(PROF_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
+    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 1, L().st);
+    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 2, L().st);
+    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
   });
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
@@ -558,7 +593,7 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   View m2 = alloc(m1.C, H, W);
   dw({m1}, dww(p + ".mlp.2"), 1, m2, true);
   conv({m2}, cw(p + ".mlp.4"), 1, 0, out, EPI_NONE, nullptr, &a);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -568,13 +603,13 @@ View Model::entropy_parameters(const std::vector<View>& ins, const std::string& 
   const int H = ins[0].H, W = ins[0].W;
   const ConvW& l3 = cw(p + ".6");
   View out = alloc(l3.Cout, H, W);
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   View a = alloc(cw(p + ".0").Cout, H, W);
   conv(ins, cw(p + ".0"), 1, 0, a, EPI_GELU);
   View b = conv1x1(a, p + ".2", 1, EPI_GELU);
   View c = conv1x1(b, p + ".4", 1, EPI_GELU);
   conv({c}, l3, 1, 0, out, EPI_NONE);
-  arena_.release(m);
+  L().arena.release(m);
   return out;
 }
 
@@ -584,7 +619,7 @@ View Model::entropy_parameters(const std::vector<View>& ins, const std::string& 
 void Model::lrp(const std::vector<View>& ins, const std::string& kind, int i, const View& yh, bool anchor) {
   const std::string p = "lrp_" + kind + "." + std::to_string(i) + ".lrp_transform";
   const int nl = cfg_.sd ? 4 : 3;
-  const size_t m = arena_.mark();
+  const size_t m = L().arena.mark();
   std::vector<View> cur = ins;
   for (int l = 0; l < nl; ++l) {
     const std::string q = p + "." + std::to_string(2 * l);
@@ -596,7 +631,7 @@ void Model::lrp(const std::vector<View>& ins, const std::string& kind, int i, co
       conv3x3(cur, q, 1, true, epi, &yh, &yh);
     }
   }
-  arena_.release(m);
+  L().arena.release(m);
 }
 
 // ------------------------------------------------------------------------------------- phases
@@ -637,7 +672,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
   const int64_t n_per = (int64_t)C * H * (W / 2);
   const View hyper_means = hyper.ch(hM, hM);
   for (int idx = 0; idx < S; ++idx) {
-    const size_t m = arena_.mark();
+    const size_t m = L().arena.mark();
     View ysl = yhat.ch(idx * C, C);
     View inter, chan, pa;
     if (idx == 0) {
@@ -653,14 +688,14 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       Q.C = C;
       Q.H = H;
       Q.W = W;
-      Q.B = B_;
+      Q.B = L().B;
       Q.yh = ysl.p;
       Q.yh_bs = ysl.bs;
       Q.table = scale_table_;
       Q.ntable = 64;
-      Q.vbr = vbr_on_ ? 1 : 0;
-      Q.sc = vbr_sc_;
-      Q.rs = vbr_rs_;
+      Q.vbr = L().vbr_on ? 1 : 0;
+      Q.sc = L().vbr_sc;
+      Q.rs = L().vbr_rs;
       Q.phase = ph;
       View pn;
       if (ph == 1) {
@@ -681,10 +716,10 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
         int32_t* ds = d_sym;
         Q.idx = di;
         Q.sym = ds;
-        if (!dry_) {
-          phase_indexes(Q, st_);
-          dec->run(n_per, st_, di, ds);
-          phase_dequant(Q, st_);
+        if (!L().dry) {
+          phase_indexes(Q, L().st);
+          dec->run(n_per, L().st, di, ds);
+          phase_dequant(Q, L().st);
         }
       } else {
         Q.y = y->p + (int64_t)idx * C * HW;
@@ -696,15 +731,15 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.params_a_bs = pa.bs;
         }
         if (mode == Mode::Encode) {
-          Q.sym = d_sym + (int64_t)phase_id * B_ * n_per;
-          Q.idx = d_idx + (int64_t)phase_id * B_ * n_per;
+          Q.sym = d_sym + (int64_t)phase_id * L().B * n_per;
+          Q.idx = d_idx + (int64_t)phase_id * L().B * n_per;
         }
-        timed(PROF_ELEM, 0.0, 4.0 * B_ * C * HW * 5, [&] { quant_phase(Q, st_); });
+        timed(PROF_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); });
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
       lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
     }
-    arena_.release(m);
+    L().arena.release(m);
   }
 }
 
@@ -724,89 +759,148 @@ void Model::eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym) {
   P.C = z.C;
   P.H = z.H;
   P.W = z.W;
-  P.B = B_;
-  timed(PROF_ELEM, 0.0, 12.0 * B_ * z.C * z.H * z.W, [&] { eb_forward(P, st_); });
+  P.B = L().B;
+  timed(PROF_ELEM, 0.0, 12.0 * L().B * z.C * z.H * z.W, [&] { eb_forward(P, L().st); });
 }
 
 template <class F>
 void Model::planned(int B, hipStream_t st, F&& body) {
-  B_ = B;
-  st_ = st;
-  dry_ = true;
-  arena_.begin(true);
+  Lane& l = L();
+  l.B = B;
+  if (st) l.st = st;
+  l.dry = true;
+  l.arena.begin(true);
   body();
-  const size_t need = arena_.peak();
-  dry_ = false;
-  arena_.ensure(need + (1 << 20));
-  arena_.begin(false);
+  const size_t need = l.arena.peak();
+  l.dry = false;
+  l.arena.ensure(need + (1 << 20));
+  l.arena.begin(false);
   body();
 }
 
 void Model::ensure_host(size_t n) {
-  if (n <= h_cap_) return;
-  if (h_sym_) HIP_OK(hipHostFree(h_sym_));
-  if (h_idx_) HIP_OK(hipHostFree(h_idx_));
-  HIP_OK(hipHostMalloc(&h_sym_, n * sizeof(int32_t)));
-  HIP_OK(hipHostMalloc(&h_idx_, n * sizeof(int32_t)));
-  h_cap_ = n;
+  Lane& l = L();
+  if (n <= l.h_cap) return;
+  if (l.h_sym) HIP_OK(hipHostFree(l.h_sym));
+  if (l.h_idx) HIP_OK(hipHostFree(l.h_idx));
+  l.h_sym = l.h_idx = nullptr;
+  HIP_OK(hipHostMalloc(&l.h_sym, n * sizeof(int32_t)));
+  HIP_OK(hipHostMalloc(&l.h_idx, n * sizeof(int32_t)));
+  l.h_cap = n;
+}
+
+void Model::set_vbr(float scale) {
+  Lane& l = L();
+  l.vbr_on = cfg_.vbr;
+  l.vbr_sc = scale;
+  l.vbr_rs = 1.0f / scale;
 }
 
 hipEvent_t Model::next_event() {
-  if (ev_used_ == ev_pool_.size()) {
+  Lane& l = L();
+  if (l.ev_used == l.ev_pool.size()) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
-    ev_pool_.push_back(e);
+    l.ev_pool.push_back(e);
   }
-  return ev_pool_[ev_used_++];
+  return l.ev_pool[l.ev_used++];
 }
 
 template <class F>
 void Model::timed(int cat, double flops, double bytes, F&& launch) {
-  if (dry_) return;
-  if (!prof_) {
+  Lane& l = L();
+  if (l.dry) return;
+  if (!l.prof) {
     launch();
     return;
   }
-  ProfRec r;
+  Lane::ProfRec r;
   r.a = next_event();
   r.b = next_event();
   r.cat = cat;
   r.flops = flops;
   r.bytes = bytes;
-  HIP_OK(hipEventRecord(r.a, st_));
+  HIP_OK(hipEventRecord(r.a, l.st));
   launch();
-  HIP_OK(hipEventRecord(r.b, st_));
-  recs_.push_back(r);
+  HIP_OK(hipEventRecord(r.b, l.st));
+  l.recs.push_back(r);
 }
 
 ProfStat Model::profile_read(int cat) {
   ProfStat s;
-  std::vector<ProfRec> keep;
-  for (auto& r : recs_) {
-    if (r.cat != cat) {
-      keep.push_back(r);
-      continue;
+  for (auto& lp : lanes_) {
+    Lane& l = *lp;
+    std::vector<Lane::ProfRec> keep;
+    for (auto& r : l.recs) {
+      if (r.cat != cat) {
+        keep.push_back(r);
+        continue;
+      }
+      HIP_OK(hipEventSynchronize(r.b));
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
+      s.launches += 1;
+      s.ms += ms;
+      s.flops += r.flops;
+      s.bytes += r.bytes;
     }
-    HIP_OK(hipEventSynchronize(r.b));
-    float ms = 0.f;
-    HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
-    s.launches += 1;
-    s.ms += ms;
-    s.flops += r.flops;
-    s.bytes += r.bytes;
+    l.recs.swap(keep);
+    if (l.recs.empty()) l.ev_used = 0;
   }
-  recs_.swap(keep);
-  if (recs_.empty()) ev_used_ = 0;
   return s;
+}
+
+template <class F>
+void Model::over_lanes(int B, hipStream_t caller, F&& fn) {
+  const int nl = std::max(1, std::min(nlanes_, B));
+  hipEvent_t ready;
+  HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(ready, caller));  // inputs produced on the caller's stream
+  std::vector<std::exception_ptr> errs(nl);
+  std::vector<std::thread> th;
+  int first = 0;
+  for (int i = 0; i < nl; ++i) {
+    const int cnt = B / nl + (i < B % nl ? 1 : 0);
+    Lane& l = lane(i);
+    HIP_OK(hipStreamWaitEvent(l.st, ready, 0));
+    th.emplace_back([&, i, first, cnt, &l = l] {
+      tl_lane_ = &l;
+      try {
+        fn(l, first, cnt);
+      } catch (...) {
+        errs[i] = std::current_exception();
+      }
+      tl_lane_ = nullptr;
+    });
+    first += cnt;
+  }
+  for (auto& t : th) t.join();
+  for (int i = 0; i < nl; ++i) {  // outputs visible to the caller's stream
+    hipEvent_t done;
+    HIP_OK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(done, lanes_[i]->st));
+    HIP_OK(hipStreamWaitEvent(caller, done, 0));
+    HIP_OK(hipEventDestroy(done));
+  }
+  HIP_OK(hipEventDestroy(ready));
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
 }
 
 // ------------------------------------------------------------------------------------- entry points
 void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
                     hipStream_t st) {
   MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64 (pad like utils/testing.py:130-137)");
-  vbr_on_ = cfg_.vbr;
-  vbr_sc_ = vbr_scale;
-  vbr_rs_ = 1.0f / vbr_scale;
+  // forward() runs on the caller's stream in lane 0 (torch-ordered, capturable)
+  Lane& l = lane(0);
+  hipStream_t own = l.st;
+  tl_lane_ = &l;
+  struct Restore {
+    Lane& l;
+    hipStream_t s;
+    ~Restore() { l.st = s; tl_lane_ = nullptr; }
+  } restore{l, own};
+  set_vbr(vbr_scale);
   planned(B, st, [&] {
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
@@ -826,18 +920,28 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
 void Model::compress(const float* x, int B, int H, int W, float vbr_scale, hipStream_t st) {
   MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64");
   MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
-  vbr_on_ = cfg_.vbr;
-  vbr_sc_ = vbr_scale;
-  vbr_rs_ = 1.0f / vbr_scale;
+  enc_all_.assign(B, EncodedImage{});
+  const int64_t img = (int64_t)3 * H * W;
+  over_lanes(B, st, [&](Lane& l, int first, int cnt) {
+    set_vbr(vbr_scale);
+    compress_lane(x + first * img, cnt, H, W);
+    for (int b = 0; b < cnt; ++b) enc_all_[first + b] = std::move(l.enc[b]);
+  });
+}
+
+// mlicpp.py:199-290 for the lane's images: network on the lane stream, then one host thread per
+// image runs the rANS coder over that image's 20 phase streams (+ the z stream)
+void Model::compress_lane(const float* x, int B, int H, int W) {
+  Lane& l = L();
   const int h = H / 16, w = W / 16, hz = H / 64, wz = W / 64;
   const int64_t n_per = (int64_t)cfg_.C * h * (w / 2);
   const int nph = 2 * cfg_.S;
   const int64_t ny = (int64_t)nph * B * n_per, nz = (int64_t)B * cfg_.N * hz * wz;
   int32_t *d_sym = nullptr, *d_idx = nullptr, *d_zsym = nullptr;
-  planned(B, st, [&] {
-    d_sym = reinterpret_cast<int32_t*>(arena_.alloc(ny));
-    d_idx = reinterpret_cast<int32_t*>(arena_.alloc(ny));
-    d_zsym = reinterpret_cast<int32_t*>(arena_.alloc(nz));
+  planned(B, nullptr, [&] {
+    d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
+    d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
+    d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(nz));
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
     View z = h_a(y);
@@ -847,15 +951,15 @@ void Model::compress(const float* x, int B, int H, int W, float vbr_scale, hipSt
     View yhat = alloc(cfg_.M, y.H, y.W);
     slice_loop(Mode::Encode, hyper, &y, yhat, nullptr, d_sym, d_idx, nullptr);
   });
-  ensure_host((size_t)(2 * ny + nz));
-  int32_t* hs = h_sym_;
-  int32_t* hi = h_idx_;
-  int32_t* hz_ = h_sym_ + ny;
-  HIP_OK(hipMemcpyAsync(hs, d_sym, ny * 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(hi, d_idx, ny * 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(hz_, d_zsym, nz * 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  enc_.assign(B, EncodedImage{});
+  ensure_host((size_t)(ny + nz));
+  int32_t* hs = l.h_sym;
+  int32_t* hi = l.h_idx;
+  int32_t* hzs = l.h_sym + ny;
+  HIP_OK(hipMemcpyAsync(hs, d_sym, ny * 4, hipMemcpyDeviceToHost, l.st));
+  HIP_OK(hipMemcpyAsync(hi, d_idx, ny * 4, hipMemcpyDeviceToHost, l.st));
+  HIP_OK(hipMemcpyAsync(hzs, d_zsym, nz * 4, hipMemcpyDeviceToHost, l.st));
+  HIP_OK(hipStreamSynchronize(l.st));
+  l.enc.assign(B, EncodedImage{});
   const int64_t zper = (int64_t)cfg_.N * hz * wz;
   auto work = [&](int b) {
     // y: phases in order, this image's part of each ([phase][B][n_per] on device)
@@ -864,54 +968,73 @@ void Model::compress(const float* x, int B, int H, int W, float vbr_scale, hipSt
       std::memcpy(s.data() + k * n_per, hs + ((int64_t)k * B + b) * n_per, n_per * 4);
       std::memcpy(ix.data() + k * n_per, hi + ((int64_t)k * B + b) * n_per, n_per * 4);
     }
-    enc_[b].y = rans_encode(s.data(), ix.data(), (int64_t)s.size(), gc_);
-    enc_[b].y_sym = std::move(s);
-    enc_[b].y_idx = std::move(ix);
-    enc_[b].z_sym.assign(hz_ + b * zper, hz_ + (b + 1) * zper);
+    l.enc[b].y = rans_encode(s.data(), ix.data(), (int64_t)s.size(), gc_);
+    l.enc[b].y_sym = std::move(s);
+    l.enc[b].y_idx = std::move(ix);
+    l.enc[b].z_sym.assign(hzs + b * zper, hzs + (b + 1) * zper);
     // z: EntropyBottleneck._build_indexes -> channel index, C-order over [C, hz, wz]
     std::vector<int32_t> zi(zper);
     for (int64_t i = 0; i < zper; ++i) zi[i] = (int32_t)(i / ((int64_t)hz * wz));
-    enc_[b].z = rans_encode(hz_ + b * zper, zi.data(), zper, eb_);
+    l.enc[b].z = rans_encode(hzs + b * zper, zi.data(), zper, eb_);
   };
-  if (B == 1) work(0);
-  else {
+  if (B == 1) {
+    work(0);
+  } else {
     std::vector<std::thread> th;
-    for (int b = 0; b < B; ++b) th.emplace_back(work, b);
+    std::vector<std::exception_ptr> errs(B);
+    for (int b = 0; b < B; ++b)
+      th.emplace_back([&, b] {
+        try {
+          work(b);
+        } catch (...) {
+          errs[b] = std::current_exception();
+        }
+      });
     for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
   }
 }
 
 void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
                        int B, int hz, int wz, float* x_hat, float vbr_scale, hipStream_t st) {
   MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
-  vbr_on_ = cfg_.vbr;
-  vbr_sc_ = vbr_scale;
-  vbr_rs_ = 1.0f / vbr_scale;
+  const int64_t img = (int64_t)3 * 64 * hz * 64 * wz;
+  over_lanes(B, st, [&](Lane& l, int first, int cnt) {
+    set_vbr(vbr_scale);
+    decompress_lane(y + first, ylen + first, z + first, zlen + first, cnt, hz, wz, x_hat + first * img);
+  });
+}
+
+// mlicpp.py:292-378 for the lane's images: z decoded on the host, then 20 phases of
+// (network -> indexes D2H -> per-image host rANS decode -> symbols H2D -> dequantise)
+void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z,
+                            const size_t* zlen, int B, int hz, int wz, float* x_hat) {
+  Lane& l = L();
   const int h = hz * 4, w = wz * 4;
   const int64_t n_per = (int64_t)cfg_.C * h * (w / 2);
   const int64_t zper = (int64_t)cfg_.N * hz * wz;
   ensure_host((size_t)std::max<int64_t>(B * n_per, B * zper));
-  // z first (host decode, before the network needs it)
   {
     std::vector<int32_t> zi(zper);
     for (int64_t i = 0; i < zper; ++i) zi[i] = (int32_t)(i / ((int64_t)hz * wz));
     for (int b = 0; b < B; ++b) {
       RansDecoderState d;
       d.set_stream(z[b], zlen[b]);
-      d.decode(zi.data(), zper, eb_, h_sym_ + b * zper);
+      d.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
     }
   }
-  PhaseDecoder dec(B, y, ylen, &gc_, h_sym_, h_idx_);
-  const int32_t* hz_sym = h_sym_;
-  planned(B, st, [&] {
-    int32_t* d_zsym = reinterpret_cast<int32_t*>(arena_.alloc(B * zper));
-    int32_t* d_sym = reinterpret_cast<int32_t*>(arena_.alloc(B * n_per));
-    int32_t* d_idx = reinterpret_cast<int32_t*>(arena_.alloc(B * n_per));
+  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx);
+  const int32_t* hz_sym = l.h_sym;
+  planned(B, nullptr, [&] {
+    int32_t* d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(B * zper));
+    int32_t* d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(B * n_per));
+    int32_t* d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(B * n_per));
     View zh = alloc(cfg_.N, hz, wz);
-    if (!dry_) {
-      HIP_OK(hipMemcpyAsync(d_zsym, hz_sym, B * zper * 4, hipMemcpyHostToDevice, st_));
-      eb_dequant(d_zsym, rw("entropy_bottleneck.quantiles"), zh.p, cfg_.N, hz * wz, B_, st_);
-      HIP_OK(hipStreamSynchronize(st_));  // h_sym_ is reused by the phase decoder
+    if (!l.dry) {
+      HIP_OK(hipMemcpyAsync(d_zsym, hz_sym, B * zper * 4, hipMemcpyHostToDevice, l.st));
+      eb_dequant(d_zsym, rw("entropy_bottleneck.quantiles"), zh.p, cfg_.N, hz * wz, B, l.st);
+      HIP_OK(hipStreamSynchronize(l.st));  // the z symbols' host buffer is reused by the phase decoder
     }
     View hyper = h_s(zh);
     View yhat = alloc(cfg_.M, h, w);
@@ -924,6 +1047,14 @@ void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_
 // module-level entry points (tests): which in {local, chan, inter, intra, epa, epn, lrpa, lrpn, g_a, h_a, h_s, g_s, rbu}
 void Model::run_module(const std::string& which, int i, const float* in0, const float* in1, int B, int Cin, int H,
                        int W, float* out, hipStream_t st) {
+  Lane& l = lane(0);
+  hipStream_t own = l.st;
+  tl_lane_ = &l;
+  struct Restore {
+    Lane& l;
+    hipStream_t s;
+    ~Restore() { l.st = s; tl_lane_ = nullptr; }
+  } restore{l, own};
   planned(B, st, [&] {
     View a{const_cast<float*>(in0), Cin, H, W, (int64_t)Cin * H * W};
     View r;
@@ -947,11 +1078,11 @@ void Model::run_module(const std::string& which, int i, const float* in0, const 
     } else if (which == "lrpn") {
       // in0 = LRP input, in1 = residual slice (copied to out first); out = res + mask(0.5 tanh(lrp(x)))
       View o{out, cfg_.C, H, W, (int64_t)cfg_.C * H * W};
-      if (!dry_) HIP_OK(hipMemcpyAsync(out, in1, sizeof(float) * B * o.bs, hipMemcpyDeviceToDevice, st_));
+      if (!L().dry) HIP_OK(hipMemcpyAsync(out, in1, sizeof(float) * B * o.bs, hipMemcpyDeviceToDevice, L().st));
       lrp({a}, "nonanchor", i, o, false);
       return;
     } else throw Error("mlic: unknown module " + which);
-    if (!dry_) HIP_OK(hipMemcpyAsync(out, r.p, sizeof(float) * B * r.bs, hipMemcpyDeviceToDevice, st_));
+    if (!L().dry) HIP_OK(hipMemcpyAsync(out, r.p, sizeof(float) * B * r.bs, hipMemcpyDeviceToDevice, L().st));
   });
 }
 

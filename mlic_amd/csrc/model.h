@@ -64,6 +64,36 @@ struct EncodedImage {
   std::vector<int32_t> y_sym, y_idx, z_sym;  // the coder inputs, in coder order (tests / tooling)
 };
 
+class PhaseDecoder;
+
+// Per-call execution state.  A Model owns several lanes so that a batch can be split over host
+// threads, each driving its own HIP stream: one lane's host entropy coding overlaps another
+// lane's kernels (weights and entropy tables are shared, read-only).
+struct Lane {
+  Arena arena;
+  hipStream_t st = nullptr;
+  bool own_stream = false;
+  int B = 0;
+  bool dry = false;
+  float vbr_sc = 1.0f, vbr_rs = 1.0f;
+  bool vbr_on = false;
+  std::vector<EncodedImage> enc;
+  int32_t* h_sym = nullptr;
+  int32_t* h_idx = nullptr;
+  size_t h_cap = 0;
+  // profiling
+  struct ProfRec {
+    hipEvent_t a, b;
+    int cat;
+    double flops, bytes;
+  };
+  bool prof = false;
+  std::vector<ProfRec> recs;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  ~Lane();
+};
+
 class Model {
  public:
   Model(const std::string& name, int n, const char* const* names, const float* const* ptrs, const int64_t* shapes,
@@ -76,7 +106,7 @@ class Model {
                hipStream_t st);
   // compress(): network + rANS; results readable with encoded(b)
   void compress(const float* x, int B, int H, int W, float vbr_scale, hipStream_t st);
-  const EncodedImage& encoded(int b) const { return enc_.at(b); }
+  const EncodedImage& encoded(int b) const { return enc_all_.at(b); }
   // decompress(): y/z byte streams per image -> x_hat [B,3,4*16*hz,4*16*wz]
   void decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen, int B,
                   int hz, int wz, float* x_hat, float vbr_scale, hipStream_t st);
@@ -84,8 +114,10 @@ class Model {
     gc_ = gc;
     eb_ = eb;
   }
-  size_t arena_bytes() const { return arena_.capacity(); }
-  void set_profiling(bool on) { prof_ = on; }
+  size_t arena_bytes() const;
+  void set_profiling(bool on);
+  void set_lanes(int n);
+  int lanes() const { return nlanes_; }
   ProfStat profile_read(int cat);  // synchronises the recorded events; clears that category
   size_t weight_bytes() const { return wbytes_; }
   // module-level entry points for tests
@@ -102,32 +134,23 @@ class Model {
   size_t wbytes_ = 0;
   float* scale_table_ = nullptr;
   int* rel_index_ = nullptr;
-  Arena arena_;
-  // per-call state
-  hipStream_t st_ = nullptr;
-  int B_ = 0;
-  bool dry_ = false;
-  float vbr_sc_ = 1.0f, vbr_rs_ = 1.0f;
-  bool vbr_on_ = false;
   CdfTables gc_, eb_;
-  std::vector<EncodedImage> enc_;
-  // profiling
-  struct ProfRec {
-    hipEvent_t a, b;
-    int cat;
-    double flops, bytes;
-  };
+  std::vector<EncodedImage> enc_all_;
+  std::vector<std::unique_ptr<Lane>> lanes_;
+  int nlanes_ = 2;
   bool prof_ = false;
-  std::vector<ProfRec> recs_;
-  std::vector<hipEvent_t> ev_pool_;
-  size_t ev_used_ = 0;
+  static thread_local Lane* tl_lane_;
+  Lane& L() const { return *tl_lane_; }
+  Lane& lane(int i);
   hipEvent_t next_event();
   template <class F>
   void timed(int cat, double flops, double bytes, F&& launch);
-  // host staging for the coder
-  int32_t* h_sym_ = nullptr;
-  int32_t* h_idx_ = nullptr;
-  size_t h_cap_ = 0;
+  // run fn(lane, first_image, count) over the batch split across lanes (host threads)
+  template <class F>
+  void over_lanes(int B, hipStream_t caller, F&& fn);
+  void compress_lane(const float* x, int B, int H, int W);
+  void decompress_lane(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
+                       int B, int hz, int wz, float* x_hat);
 
   // -- weights
   const ConvW& cw(const std::string& k) const;
@@ -165,6 +188,7 @@ class Model {
   template <class F>
   void planned(int B, hipStream_t st, F&& body);
   void ensure_host(size_t n);
+  void set_vbr(float scale);
 };
 
 }  // namespace mlic

@@ -20,19 +20,46 @@ constexpr int PRECISION = 16;
 constexpr int BYPASS_PRECISION = 4;
 constexpr int MAX_BYPASS_VAL = (1 << BYPASS_PRECISION) - 1;
 
-struct Sym {
-  uint16_t start;
-  uint16_t range;
-  bool bypass;
+struct Sym {  // a coded symbol: table*stride + value (regular) or the 4-bit bypass value | flag
+  uint32_t v;
 };
+constexpr uint32_t BYPASS_FLAG = 0x80000000u;
 
-inline void enc_put(uint64_t& x, uint32_t*& ptr, uint32_t start, uint32_t freq, uint32_t scale_bits) {
-  const uint64_t x_max = ((RANS64_L >> scale_bits) << 32) * freq;
+inline uint64_t mulhi64(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+
+// Rans64EncSymbolInit: x' = (x / freq) * 2^16 + x % freq + start computed as
+// x + bias + q * (2^16 - freq), q = mulhi(x, rcp) >> shift == x / freq exactly (ryg_rans proof)
+EncSym make_enc_sym(uint32_t start, uint32_t freq) {
+  EncSym s;
+  s.freq = freq;
+  s.cmpl_freq = (1u << PRECISION) - freq;
+  if (freq < 2) {
+    s.rcp_freq = ~0ull;
+    s.rcp_shift = 0;
+    s.bias = start + (1u << PRECISION) - 1;
+  } else {
+    uint32_t shift = 0;
+    while (freq > (1u << shift)) shift++;
+    uint64_t x0 = freq - 1;
+    const uint64_t x1 = 1ull << (shift + 31);
+    const uint64_t t1 = x1 / freq;
+    x0 += (x1 % freq) << 32;
+    const uint64_t t0 = x0 / freq;
+    s.rcp_freq = t0 + (t1 << 32);
+    s.rcp_shift = shift - 1;
+    s.bias = start;
+  }
+  return s;
+}
+
+inline void enc_put_sym(uint64_t& x, uint32_t*& ptr, const EncSym& s) {
+  const uint64_t x_max = ((RANS64_L >> PRECISION) << 32) * s.freq;
   if (x >= x_max) {
     *--ptr = (uint32_t)x;
     x >>= 32;
   }
-  x = ((x / freq) << scale_bits) + (x % freq) + start;
+  const uint64_t q = mulhi64(x, s.rcp_freq) >> s.rcp_shift;
+  x = x + s.bias + q * s.cmpl_freq;
 }
 
 inline void enc_put_bits(uint64_t& x, uint32_t*& ptr, uint32_t val, uint32_t nbits) {
@@ -47,46 +74,45 @@ inline void enc_put_bits(uint64_t& x, uint32_t*& ptr, uint32_t val, uint32_t nbi
 }  // namespace
 
 std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t) {
+  if (t.enc.empty()) throw std::runtime_error("rans: tables not prepared");
   std::vector<Sym> syms;
   syms.reserve((size_t)n + 16);
   for (int64_t i = 0; i < n; ++i) {
     const int32_t ci = indexes[i];
     if (ci < 0 || ci >= t.n) throw std::runtime_error("rans: cdf index out of range");
-    const int32_t* cdf = t.cdf.data() + (int64_t)ci * t.stride;
     const int32_t max_value = t.length[ci] - 2;
     int32_t value = symbols[i] - t.offset[ci];
     uint32_t raw = 0;
     if (value < 0) {
-      raw = (uint32_t)(-2 * value - 1);
+      raw = (uint32_t)(-2 * (int64_t)value - 1);
       value = max_value;
     } else if (value >= max_value) {
-      raw = (uint32_t)(2 * (value - max_value));
+      raw = (uint32_t)(2 * ((int64_t)value - max_value));
       value = max_value;
     }
-    syms.push_back({(uint16_t)cdf[value], (uint16_t)(cdf[value + 1] - cdf[value]), false});
+    syms.push_back({(uint32_t)(ci * t.stride + value)});
     if (value == max_value) {
       int32_t nb = 0;
       while (nb < 8 && (raw >> (nb * BYPASS_PRECISION)) != 0) ++nb;
       int32_t v = nb;
       while (v >= MAX_BYPASS_VAL) {
-        syms.push_back({(uint16_t)MAX_BYPASS_VAL, (uint16_t)(MAX_BYPASS_VAL + 1), true});
+        syms.push_back({BYPASS_FLAG | (uint32_t)MAX_BYPASS_VAL});
         v -= MAX_BYPASS_VAL;
       }
-      syms.push_back({(uint16_t)v, (uint16_t)(v + 1), true});
-      for (int32_t j = 0; j < nb; ++j) {
-        const uint32_t bv = (raw >> (j * BYPASS_PRECISION)) & MAX_BYPASS_VAL;
-        syms.push_back({(uint16_t)bv, (uint16_t)(bv + 1), true});
-      }
+      syms.push_back({BYPASS_FLAG | (uint32_t)v});
+      for (int32_t j = 0; j < nb; ++j)
+        syms.push_back({BYPASS_FLAG | ((raw >> (j * BYPASS_PRECISION)) & MAX_BYPASS_VAL)});
     }
   }
   std::vector<uint32_t> out(syms.size() + 4, 0xCCCCCCCCu);
   uint32_t* end = out.data() + out.size();
   uint32_t* ptr = end;
   uint64_t x = RANS64_L;
+  const EncSym* es = t.enc.data();
   for (size_t k = syms.size(); k-- > 0;) {
-    const Sym& s = syms[k];
-    if (!s.bypass) enc_put(x, ptr, s.start, s.range, PRECISION);
-    else enc_put_bits(x, ptr, s.start, BYPASS_PRECISION);
+    const uint32_t v = syms[k].v;
+    if (!(v & BYPASS_FLAG)) enc_put_sym(x, ptr, es[v]);
+    else enc_put_bits(x, ptr, v & ~BYPASS_FLAG, BYPASS_PRECISION);
   }
   ptr -= 2;  // flush
   ptr[0] = (uint32_t)(x >> 0);
@@ -117,8 +143,14 @@ void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables
     const int32_t len = t.length[ci];
     const int32_t max_value = len - 2;
     const uint32_t cum = (uint32_t)(state_ & mask);
-    // first entry > cum, minus one (cdf is strictly increasing)
-    const int32_t s = (int32_t)(std::upper_bound(cdf, cdf + len, (int32_t)cum) - cdf) - 1;
+    // s = (first entry > cum) - 1; the bucket table gives a start at or below s (cdf strictly increasing)
+    int32_t s;
+    if (!t.lut.empty()) {
+      s = t.lut[(size_t)ci * (1u << CdfTables::LUT_BITS) + (cum >> (PRECISION - CdfTables::LUT_BITS))];
+      while (s < len - 1 && (uint32_t)cdf[s + 1] <= cum) ++s;
+    } else {
+      s = (int32_t)(std::upper_bound(cdf, cdf + len, (int32_t)cum) - cdf) - 1;
+    }
     if (s < 0 || s > max_value) throw std::runtime_error("rans: corrupt stream");
     const uint32_t start = (uint32_t)cdf[s], freq = (uint32_t)(cdf[s + 1] - cdf[s]);
     uint64_t x = freq * (state_ >> PRECISION) + (state_ & mask) - start;
@@ -148,6 +180,28 @@ void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables
       else value += max_value;
     }
     out[i] = value + t.offset[ci];
+  }
+}
+
+void CdfTables::prepare() {
+  enc.assign((size_t)n * stride, EncSym{~0ull, 1, 0, 0, 0});
+  const size_t L = (size_t)1 << LUT_BITS;
+  lut.assign((size_t)n * L, 0);
+  for (int k = 0; k < n; ++k) {
+    const int32_t* c = cdf.data() + (size_t)k * stride;
+    const int len = length[k];
+    if (len < 3 || len > stride || c[0] != 0 || c[len - 1] != (1 << PRECISION))
+      throw std::runtime_error("rans: malformed cdf table");
+    for (int v = 0; v + 1 < len; ++v) {
+      if (c[v + 1] <= c[v]) throw std::runtime_error("rans: cdf not strictly increasing");
+      enc[(size_t)k * stride + v] = make_enc_sym((uint32_t)c[v], (uint32_t)(c[v + 1] - c[v]));
+    }
+    int s = 0;
+    for (size_t b = 0; b < L; ++b) {
+      const uint32_t lo = (uint32_t)(b << (PRECISION - LUT_BITS));
+      while (s < len - 2 && (uint32_t)c[s + 1] <= lo) ++s;
+      lut[(size_t)k * L + b] = (uint16_t)s;
+    }
   }
 }
 

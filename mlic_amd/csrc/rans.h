@@ -8,6 +8,11 @@
 
 namespace mlic {
 
+struct EncSym {  // ryg_rans Rans64EncSymbol: exact division-free encode step
+  uint64_t rcp_freq;
+  uint32_t freq, bias, cmpl_freq, rcp_shift;
+};
+
 struct CdfTables {
   // table k: cdf[k * stride .. + length[k]]  (length includes the two sentinels, as compressai)
   std::vector<int32_t> cdf;
@@ -16,6 +21,11 @@ struct CdfTables {
   int stride = 0;
   int n = 0;
   bool empty() const { return n == 0; }
+  // derived (prepare()): per-symbol encoder records and a 2^LUT_BITS decode bucket table
+  static constexpr int LUT_BITS = 10;
+  std::vector<EncSym> enc;       // [n][stride]
+  std::vector<uint16_t> lut;     // [n][1 << LUT_BITS]: first symbol s with cdf[s+1] > bucket start
+  void prepare();
 };
 
 // Encodes symbols[i] with table indexes[i]; returns the byte string (little-endian u32 words).

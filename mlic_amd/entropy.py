@@ -109,11 +109,11 @@ def rans_encode(symbols, indexes, cdf, length, offset) -> bytes:
     ix = np.ascontiguousarray(np.asarray(indexes).reshape(-1), dtype=np.int32)
     cdf, length, offset = _tab_args(cdf, length, offset)
     cap = 4 * (2 * s.size + 16) + 64
-    buf = (C.c_uint8 * cap)()
+    buf = C.create_string_buffer(cap)
     written = C.c_size_t(0)
     _lib.call("mlic_rans_encode", s.ctypes.data, ix.ctypes.data, s.size, cdf.ctypes.data, length.ctypes.data,
               offset.ctypes.data, cdf.shape[0], cdf.shape[1], buf, cap, C.byref(written))
-    return bytes(buf[: written.value])
+    return C.string_at(buf, written.value)
 
 
 def rans_decode(data: bytes, indexes, cdf, length, offset) -> np.ndarray:

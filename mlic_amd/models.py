@@ -145,10 +145,18 @@ class MLICPlusPlus(nn.Module):
         self._handle = h
         self._handle_key = key
         self._tables_pushed = None
+        if getattr(self, "_lanes", None):
+            _lib.call("mlic_set_lanes", h, self._lanes)
         return h
 
     def _vbr_scale(self, **kw) -> float:
         return 1.0
+
+    def set_lanes(self, n: int):
+        """Host threads x HIP streams used by compress()/decompress() (results do not depend on it)."""
+        self._lanes = int(n)
+        if self._handle is not None:
+            _lib.call("mlic_set_lanes", self._handle, self._lanes)
 
     @staticmethod
     def _stream():
@@ -239,11 +247,11 @@ class MLICPlusPlus(nn.Module):
         for b in range(B):
             yl, zl = C.c_size_t(), C.c_size_t()
             _lib.call("mlic_encoded_size", h, b, C.byref(yl), C.byref(zl))
-            yb = (C.c_uint8 * max(1, yl.value))()
-            zb = (C.c_uint8 * max(1, zl.value))()
+            yb = C.create_string_buffer(max(1, yl.value))
+            zb = C.create_string_buffer(max(1, zl.value))
             _lib.call("mlic_encoded_copy", h, b, yb, zb)
-            ys.append(bytes(yb[: yl.value]))
-            zs.append(bytes(zb[: zl.value]))
+            ys.append(C.string_at(yb, yl.value))
+            zs.append(C.string_at(zb, zl.value))
         torch.cuda.synchronize(x.device)
         return {"strings": [ys, zs], "shape": torch.Size([H // 64, W // 64]), "cost_time": time.time() - t0}
 

@@ -164,6 +164,27 @@ def test_roundtrip_bitexact(name, B, H, W, s):
     assert torch.equal(d["x_hat"], f["x_hat"])
 
 
+def test_lanes_do_not_change_bitstreams():
+    """The batch split over lanes (host threads x HIP streams) is a scheduling choice only."""
+    net = net_for("MLICPP_S")
+    net.update()
+    x = torch.cat([synthetic.synth_image(128, 192, 40 + i) for i in range(3)]).to(DEV)
+    outs = []
+    for lanes in (1, 2, 3):
+        net.set_lanes(lanes)
+        c = net.compress(x)
+        d = net.decompress(c["strings"], c["shape"])
+        outs.append((c["strings"], d["x_hat"].cpu()))
+    net.set_lanes(2)
+    for s_, xh in outs[1:]:
+        assert s_ == outs[0][0]
+        assert torch.equal(xh, outs[0][1])
+    # and every image's stream equals the one it gets when coded alone
+    for i in range(3):
+        ci = net.compress(x[i:i + 1])
+        assert ci["strings"][0][0] == outs[0][0][0][i] and ci["strings"][1][0] == outs[0][0][1][i]
+
+
 def test_1080p_parity_and_roundtrip():
     """BASELINE config 2 size: 1920x1088 MLICPP_L, bpp / PSNR vs the CPU oracle, and the
     size-independent round-trip invariant at full size."""
