@@ -29,8 +29,14 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-CATS = ["conv_mfma_kernel<64,64>", "conv_mfma_kernel<64,128>", "conv_mfma_kernel<128,64>",
-        "conv_mfma_kernel<128,128>", "dw3x3_kernel", "local_attn_kernel", "linear_attention", "elementwise"]
+CONV32 = ["conv_mfma_kernel<64,64>", "conv_mfma_kernel<64,128>", "conv_mfma_kernel<128,64>",
+          "conv_mfma_kernel<128,128>"]
+CONVX3 = ["conv_f16x3_kernel<64,64>", "conv_f16x3_kernel<64,128>", "conv_f16x3_kernel<128,64>",
+          "conv_f16x3_kernel<128,128>"]
+CATS = CONV32 + CONVX3 + ["dw3x3_kernel", "local_attn_kernel", "linear_attention", "elementwise"]
+# dense peak of the arithmetic each conv kernel runs on (MI355X_MICROARCH.md): fp32 MFMA 157.3 TF;
+# f16x3 issues 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of fp32-equivalent work
+PEAK = {**{k: 157.3 for k in CONV32}, **{k: 2500.0 / 3 for k in CONVX3}}
 METRIC = "images/sec (enc+dec) at 1920×1088 MLICPP_L, 1/2/4/8 GPU; bpp/PSNR Δ vs ref"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense, exact f32)
 PEAK_HBM_GBS = 8000.0
@@ -41,10 +47,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--model", default="MLICPP_L")
     ap.add_argument("--height", type=int, default=1088)
     ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("MLIC_LANES", "4")),
+                    help="host threads x HIP streams per GPU for compress/decompress")
+    ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "1")),
+                    help="dense-conv arithmetic: 1 = split-fp16 MFMA (f16x3), 0 = fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per conv launch (written by tools/pmc_traffic.py)")
@@ -105,6 +115,8 @@ def main():
     net.load_state_dict(synthetic.synth_state_dict(a.model, 0))
     net = net.to(dev).eval()
     net.update()
+    net.set_lanes(a.lanes)
+    net.set_precision(a.precision)
     B, H, W = a.batch, a.height, a.width
     x = torch.cat([synthetic.synth_image(H, W, 1000 * rank + i) for i in range(B)]).to(dev)
 
@@ -147,20 +159,22 @@ def main():
 
     # live roofline of the dominant kernel family: one extra profiled (untimed) step
     h = net._handle
+    _lib.call("mlic_set_lanes", h, 1)  # events on overlapping lanes would double-count device time
     _lib.call("mlic_set_profiling", h, 1)
     step()
     torch.cuda.synchronize()
     _lib.call("mlic_set_profiling", h, 0)
+    net.set_lanes(a.lanes)
     fam = {}
     for cat, nm in enumerate(CATS):
         n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
         _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
         fam[nm] = {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
     # dominant kernel = the conv tile instantiation with the most device time
-    dom = max(CATS[:4], key=lambda k: fam[k]["ms"])
+    dom = max(CONV32 + CONVX3, key=lambda k: fam[k]["ms"])
     conv = fam[dom]
     achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12 if conv["ms"] > 0 else 0.0
-    conv_all = {k: sum(fam[c][k] for c in CATS[:4]) for k in ("launches", "ms", "flops")}
+    conv_all = {k: sum(fam[c][k] for c in CONV32 + CONVX3) for k in ("launches", "ms", "flops")}
     traffic = None
     try:
         with open(a.traffic_json) as f:
@@ -184,14 +198,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if a.precision == 0 else "f32 (dense convs: f32 via split-fp16 MFMA, 3 terms)",
             "data": "synthetic (seeded sinusoid images, seeded conditioned weights)",
             "config": {"workload": f"{a.model} compress+decompress (full rANS bitstreams) of {W}x{H} images",
                        "model": a.model, "global_batch": B * world, "per_gpu_batch": B, "H": H, "W": W,
                        "parallelism": f"image-sharded x{world} (no cross-GPU context)"},
-            "roofline": {"bound": "mfma", "kernel": dom + " (implicit-GEMM conv, v_mfma_f32_32x32x2_f32)",
-                         "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "kernel": dom + (" (implicit-GEMM conv, 3 x v_mfma_f32_32x32x16_f16 split-fp16)"
+                                                           if "f16x3" in dom else
+                                                           " (implicit-GEMM conv, v_mfma_f32_32x32x2_f32)"),
+                         "achieved": round(achieved, 3), "peak": round(PEAK[dom], 1), "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK[dom], 4),
                          "traffic": traffic,
                          "launches_per_step": conv["launches"],
                          "avg_launch_us": round(1000 * conv["ms"] / max(1, conv["launches"]), 2),

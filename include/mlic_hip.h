@@ -67,9 +67,12 @@ int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, con
                     int B, int Cin, int H, int W, float* out);
 int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
 
-/* live kernel timing (HIP events on the executor stream): categories 0..3 conv_mfma_kernel<64,64>,
- * <64,128>, <128,64>, <128,128>; 4 depthwise; 5 local attention; 6 linear attention;
- * 7 elementwise/reductions.  read() sums and clears that category. */
+/* dense-conv arithmetic: 1 = split-fp16 MFMA "f16x3" (default; error below fp32 summation-order
+ * noise), 0 = fp32 MFMA.  Also $MLIC_PRECISION. */
+int mlic_set_precision(mlic_model* m, int precision);
+/* live kernel timing (HIP events on the executor stream): categories 0..3 conv_mfma_kernel (fp32)
+ * <64,64>, <64,128>, <128,64>, <128,128>; 4..7 conv_f16x3_kernel with the same tiles; 8 depthwise;
+ * 9 local attention; 10 linear attention; 11 elementwise/reductions.  read() sums and clears. */
 int mlic_set_profiling(mlic_model* m, int on);
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes);
 

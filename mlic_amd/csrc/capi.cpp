@@ -54,6 +54,7 @@ int mlic_create(const char* model_name, int n, const char* const* names, const f
     try {
       m->impl = new Model(model_name, n, names, ptrs, shapes, ndims, (hipStream_t)stream);
       if (const char* e = std::getenv("MLIC_LANES")) m->impl->set_lanes(std::atoi(e));
+      if (const char* e = std::getenv("MLIC_PRECISION")) m->impl->set_precision(std::atoi(e));
     } catch (...) {
       delete m;
       throw;
@@ -141,6 +142,13 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
   return guard([&] {
     *arena = m->impl->arena_bytes();
     *weights = m->impl->weight_bytes();
+  });
+}
+
+int mlic_set_precision(mlic_model* m, int precision) {
+  return guard([&] {
+    MLIC_CHECK(precision == PREC_F32 || precision == PREC_F16X3, "precision must be 0 (f32) or 1 (f16x3)");
+    m->impl->set_precision(precision);
   });
 }
 

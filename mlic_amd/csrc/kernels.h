@@ -9,6 +9,13 @@ namespace mlic {
 int conv_variant(const ConvParams& P);
 void conv_forward(const ConvParams& P, hipStream_t st);
 
+// split-fp16 ("f16x3") MFMA conv (conv_f16x3.hip): same contract, weights pre-split to
+// hi/lo fp16 [Cout][K*K][cin_pad] (cin_pad = Cin rounded up to 32)
+int conv_f16x3_variant(const ConvParams& P);
+void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
+void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad,
+                   hipStream_t st);
+
 struct DwParams {
   Seg seg[MAXSEG];
   int nseg;
@@ -87,7 +94,7 @@ void eb_dequant(const int32_t* sym, const float* quantiles, float* z_hat, int C,
 
 void pack_conv(const float* w, float* out, int Cout, int Cin, int KK, hipStream_t st);
 void gdn_prep(const float* beta, const float* gamma, const float* bb, const float* bped, const float* gb,
-              const float* gped, float* beta_eff, float* gamma_pk, int C, hipStream_t st);
+              const float* gped, float* beta_eff, float* gamma_pk, float* gamma_eff, int C, hipStream_t st);
 void local_mask(float* out, int H, int W, hipStream_t st);
 void sq_err_u8(const float* a, int64_t a_bs, const float* b, int64_t b_bs, double* out, int64_t n_per, int B,
                hipStream_t st);

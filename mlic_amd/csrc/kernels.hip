@@ -621,7 +621,8 @@ void pack_conv(const float* w, float* out, int Cout, int Cin, int KK, hipStream_
 __global__ void gdn_prep_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
                                 const float* __restrict__ bb, const float* __restrict__ bped,
                                 const float* __restrict__ gb, const float* __restrict__ gped,
-                                float* __restrict__ beta_eff, float* __restrict__ gamma_pk, int C) {
+                                float* __restrict__ beta_eff, float* __restrict__ gamma_pk,
+                                float* __restrict__ gamma_eff, int C) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < C) {
     const float v = fmaxf(beta[i], bb[0]);
@@ -630,14 +631,16 @@ __global__ void gdn_prep_kernel(const float* __restrict__ beta, const float* __r
   if (i < C * C) {
     const int co = i / C, ci = i % C;
     const float v = fmaxf(gamma[i], gb[0]);
-    gamma_pk[ci * C + co] = v * v - gped[0];
+    const float e = v * v - gped[0];
+    gamma_pk[ci * C + co] = e;
+    gamma_eff[i] = e;  // [co][ci], conv-weight layout
   }
 }
 
 void gdn_prep(const float* beta, const float* gamma, const float* bb, const float* bped, const float* gb,
-              const float* gped, float* beta_eff, float* gamma_pk, int C, hipStream_t st) {
+              const float* gped, float* beta_eff, float* gamma_pk, float* gamma_eff, int C, hipStream_t st) {
   hipLaunchKernelGGL(gdn_prep_kernel, dim3((C * C + 255) / 256), dim3(256), 0, st, beta, gamma, bb, bped, gb, gped,
-                     beta_eff, gamma_pk, C);
+                     beta_eff, gamma_pk, gamma_eff, C);
   HIP_OK(hipGetLastError());
 }
 

@@ -64,8 +64,14 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     numel[i] = e;
     total += ((size_t)e * 4 + 255) & ~(size_t)255;
   }
-  for (int i = 0; i < n; ++i)
-    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(numel[i] + shapes[i * 4]) * 4 + 512;
+  for (int i = 0; i < n; ++i) {
+    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(2 * numel[i] + shapes[i * 4]) * 4 + 1024;
+    if (ends_with(names[i], ".weight") && (ndims[i] == 4 || ndims[i] == 2)) {
+      // split fp16 copy: 2 x Cout x KK x cin_pad halves
+      const int64_t cout = shapes[i * 4], per = numel[i] / std::max<int64_t>(1, cout);
+      total += (size_t)(cout * (per + 32 * 25)) * 4 + 1024;
+    }
+  }
   total += 64 * 4 + 625 * 4 + 1024;
   char* block = nullptr;
   HIP_OK(hipMalloc(&block, total));
@@ -111,6 +117,13 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
         MLIC_CHECK(shape(i, 2) == shape(i, 3), "square kernels only");
       }
       pack_conv(ptrs[i], dst, w.Cout, w.Cin, w.K * w.K, st);
+      if (w.Cin >= 16) {  // split-fp16 copy for the f16x3 MFMA path
+        w.cin_pad = (w.Cin + 31) / 32 * 32;
+        const int64_t nh = (int64_t)w.Cout * w.K * w.K * w.cin_pad;
+        w.wh = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
+        w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
+        split_weights(ptrs[i], w.wh, w.wl, w.Cout, w.Cin, w.K * w.K, w.cin_pad, st);
+      }
       convs_[base] = w;
     } else {
       HIP_OK(hipMemcpyAsync(dst, ptrs[i], numel[i] * 4, hipMemcpyDeviceToDevice, st));
@@ -134,15 +147,22 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     const int C = shape(i, 0);
     float* beta_eff = take(C);
     float* gamma_pk = take((int64_t)C * C);
+    float* gamma_eff = take((int64_t)C * C);
     MLIC_CHECK(off <= total, "weight block");
     gdn_prep(rw(p + ".beta"), rw(p + ".gamma"), rw(p + ".beta_reparam.lower_bound.bound"),
              rw(p + ".beta_reparam.pedestal"), rw(p + ".gamma_reparam.lower_bound.bound"),
-             rw(p + ".gamma_reparam.pedestal"), beta_eff, gamma_pk, C, st);
+             rw(p + ".gamma_reparam.pedestal"), beta_eff, gamma_pk, gamma_eff, C, st);
     ConvW w;
     w.w = gamma_pk;
     w.b = beta_eff;
     w.Cin = w.Cout = C;
     w.K = 1;
+    w.cin_pad = (C + 31) / 32 * 32;
+    const int64_t nh = (int64_t)C * w.cin_pad;
+    w.wh = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
+    w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
+    MLIC_CHECK(off <= total, "weight block");
+    split_weights(gamma_eff, w.wh, w.wl, C, C, 1, w.cin_pad, st);
     convs_[p + ".__gdn"] = w;
   }
   MLIC_CHECK(off <= total, "weight block overflow");
@@ -276,7 +296,12 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
   const double outn = (double)L().B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * cin * w.K * w.K;
   const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, L().st); });
+  if (precision_ == PREC_F16X3 && w.wh) {
+    timed(PROF_CONVX3 + conv_f16x3_variant(P), flops, bytes,
+          [&] { conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, L().st); });
+  } else {
+    timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, L().st); });
+  }
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {
@@ -767,7 +792,7 @@ template <class F>
 void Model::planned(int B, hipStream_t st, F&& body) {
   Lane& l = L();
   l.B = B;
-  if (st) l.st = st;
+  (void)st;  // the stream is chosen by the caller of planned() (lane's own or the API caller's)
   l.dry = true;
   l.arena.begin(true);
   body();
@@ -900,6 +925,7 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
     hipStream_t s;
     ~Restore() { l.st = s; tl_lane_ = nullptr; }
   } restore{l, own};
+  l.st = st;  // caller's stream, including the legacy NULL stream torch uses by default
   set_vbr(vbr_scale);
   planned(B, st, [&] {
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
@@ -1055,6 +1081,7 @@ void Model::run_module(const std::string& which, int i, const float* in0, const 
     hipStream_t s;
     ~Restore() { l.st = s; tl_lane_ = nullptr; }
   } restore{l, own};
+  l.st = st;
   planned(B, st, [&] {
     View a{const_cast<float*>(in0), Cin, H, W, (int64_t)Cin * H * W};
     View r;

@@ -22,10 +22,15 @@ struct Cfg {
 Cfg config_for(const std::string& name);
 
 struct ConvW {
-  float* w = nullptr;        // packed [K*K][Cin][Cout]
+  float* w = nullptr;        // packed [K*K][Cin][Cout]            (fp32 MFMA path)
   const float* b = nullptr;  // [Cout] or null
   int Cin = 0, Cout = 0, K = 0;
+  _Float16* wh = nullptr;    // split hi/lo [Cout][K*K][cin_pad]  (f16x3 MFMA path)
+  _Float16* wl = nullptr;
+  int cin_pad = 0;
 };
+
+enum Precision : int { PREC_F32 = 0, PREC_F16X3 = 1 };
 struct DwW {
   const float* w = nullptr;  // [C][9]
   const float* b = nullptr;
@@ -51,8 +56,10 @@ class Arena {
 };
 
 // live per-kernel-family timing with HIP events on the executor's stream (bench.py roofline)
-// categories 0..3 = conv_mfma_kernel tile instantiations (see conv_forward), then the others
-enum ProfCat : int { PROF_CONV = 0, PROF_DW = 4, PROF_LOCAL = 5, PROF_LINATT = 6, PROF_ELEM = 7, PROF_NCAT = 8 };
+// categories 0..3 = conv_mfma_kernel (fp32) tile instantiations, 4..7 = conv_f16x3_kernel ones
+enum ProfCat : int {
+  PROF_CONV = 0, PROF_CONVX3 = 4, PROF_DW = 8, PROF_LOCAL = 9, PROF_LINATT = 10, PROF_ELEM = 11, PROF_NCAT = 12
+};
 struct ProfStat {
   int64_t launches = 0;
   double ms = 0, flops = 0, bytes = 0;
@@ -117,6 +124,8 @@ class Model {
   size_t arena_bytes() const;
   void set_profiling(bool on);
   void set_lanes(int n);
+  void set_precision(int p) { precision_ = p; }
+  int precision() const { return precision_; }
   int lanes() const { return nlanes_; }
   ProfStat profile_read(int cat);  // synchronises the recorded events; clears that category
   size_t weight_bytes() const { return wbytes_; }
@@ -138,6 +147,7 @@ class Model {
   std::vector<EncodedImage> enc_all_;
   std::vector<std::unique_ptr<Lane>> lanes_;
   int nlanes_ = 2;
+  int precision_ = PREC_F16X3;
   bool prof_ = false;
   static thread_local Lane* tl_lane_;
   Lane& L() const { return *tl_lane_; }

@@ -147,10 +147,18 @@ class MLICPlusPlus(nn.Module):
         self._tables_pushed = None
         if getattr(self, "_lanes", None):
             _lib.call("mlic_set_lanes", h, self._lanes)
+        if getattr(self, "_precision", None) is not None:
+            _lib.call("mlic_set_precision", h, self._precision)
         return h
 
     def _vbr_scale(self, **kw) -> float:
         return 1.0
+
+    def set_precision(self, mode: int):
+        """Dense-conv arithmetic: 1 = split-fp16 MFMA "f16x3" (default), 0 = fp32 MFMA."""
+        self._precision = int(mode)
+        if self._handle is not None:
+            _lib.call("mlic_set_precision", self._handle, self._precision)
 
     def set_lanes(self, n: int):
         """Host threads x HIP streams used by compress()/decompress() (results do not depend on it)."""
