@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "1")),
                     help="dense-conv arithmetic: 1 = split-fp16 MFMA (f16x3), 0 = fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers-out", default="", help="write the per-layer conv timing table here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per conv launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -165,6 +166,14 @@ def main():
     torch.cuda.synchronize()
     _lib.call("mlic_set_profiling", h, 0)
     net.set_lanes(a.lanes)
+    if a.layers_out:
+        n = C.c_size_t()
+        _lib.call("mlic_profile_layers", h, None, 0, C.byref(n))
+        buf = C.create_string_buffer(n.value + 1)
+        _lib.call("mlic_profile_layers", h, buf, n.value + 1, C.byref(n))
+        if rank == 0:
+            with open(a.layers_out, "w") as f:
+                f.write(buf.value.decode())
     fam = {}
     for cat, nm in enumerate(CATS):
         n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()

@@ -75,6 +75,9 @@ int mlic_set_precision(mlic_model* m, int precision);
  * 9 local attention; 10 linear attention; 11 elementwise/reductions.  read() sums and clears. */
 int mlic_set_profiling(mlic_model* m, int on);
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes);
+/* tab-separated per-layer table (layer, category, launches, ms, GFLOP, TFLOP/s) of the recorded
+ * conv events, sorted by time; call before mlic_profile_read (which clears) */
+int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written);
 
 /* kernel-level entry points (bit-exact tests) */
 int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */

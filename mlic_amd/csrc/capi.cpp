@@ -2,6 +2,7 @@
 #include "../../include/mlic_hip.h"
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -168,6 +169,18 @@ int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, dou
     *ms = s.ms;
     *flops = s.flops;
     *bytes = s.bytes;
+  });
+}
+
+int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written) {
+  return guard([&] {
+    std::string s = m->impl->profile_layers();
+    *written = s.size();
+    if (buf && cap) {
+      const size_t n = std::min(cap - 1, s.size());
+      std::memcpy(buf, s.data(), n);
+      buf[n] = 0;
+    }
   });
 }
 

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 
@@ -124,6 +125,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
         w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
         split_weights(ptrs[i], w.wh, w.wl, w.Cout, w.Cin, w.K * w.K, w.cin_pad, st);
       }
+      w.name = base;
       convs_[base] = w;
     } else {
       HIP_OK(hipMemcpyAsync(dst, ptrs[i], numel[i] * 4, hipMemcpyDeviceToDevice, st));
@@ -163,6 +165,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
     MLIC_CHECK(off <= total, "weight block");
     split_weights(gamma_eff, w.wh, w.wl, C, C, 1, w.cin_pad, st);
+    w.name = p + ".__gdn";
     convs_[p + ".__gdn"] = w;
   }
   MLIC_CHECK(off <= total, "weight block overflow");
@@ -298,9 +301,9 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
   const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
   if (precision_ == PREC_F16X3 && w.wh) {
     timed(PROF_CONVX3 + conv_f16x3_variant(P), flops, bytes,
-          [&] { conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, L().st); });
+          [&] { conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, L().st); }, w.name);
   } else {
-    timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, L().st); });
+    timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, L().st); }, w.name);
   }
 }
 
@@ -832,7 +835,7 @@ hipEvent_t Model::next_event() {
 }
 
 template <class F>
-void Model::timed(int cat, double flops, double bytes, F&& launch) {
+void Model::timed(int cat, double flops, double bytes, F&& launch, const std::string& tag) {
   Lane& l = L();
   if (l.dry) return;
   if (!l.prof) {
@@ -845,10 +848,45 @@ void Model::timed(int cat, double flops, double bytes, F&& launch) {
   r.cat = cat;
   r.flops = flops;
   r.bytes = bytes;
+  r.tag = tag;
   HIP_OK(hipEventRecord(r.a, l.st));
   launch();
   HIP_OK(hipEventRecord(r.b, l.st));
   l.recs.push_back(r);
+}
+
+std::string Model::profile_layers() {
+  struct Acc {
+    int64_t n = 0;
+    double ms = 0, flops = 0, bytes = 0;
+    int cat = 0;
+  };
+  std::map<std::string, Acc> acc;
+  for (auto& lp : lanes_)
+    for (auto& r : lp->recs) {
+      if (r.tag.empty()) continue;
+      // group per-slice layers: drop the digits after the first dot-separated component index
+      HIP_OK(hipEventSynchronize(r.b));
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
+      Acc& a = acc[r.tag];
+      a.n++;
+      a.ms += ms;
+      a.flops += r.flops;
+      a.bytes += r.bytes;
+      a.cat = r.cat;
+    }
+  std::vector<std::pair<std::string, Acc>> v(acc.begin(), acc.end());
+  std::sort(v.begin(), v.end(), [](auto& x, auto& y) { return x.second.ms > y.second.ms; });
+  std::string out = "layer\tcat\tlaunches\tms\tGFLOP\tTFLOP/s\n";
+  char buf[512];
+  for (auto& kv : v) {
+    const Acc& a = kv.second;
+    std::snprintf(buf, sizeof buf, "%s\t%d\t%lld\t%.4f\t%.3f\t%.2f\n", kv.first.c_str(), a.cat, (long long)a.n, a.ms,
+                  a.flops / 1e9, a.ms > 0 ? a.flops / (a.ms * 1e-3) / 1e12 : 0.0);
+    out += buf;
+  }
+  return out;
 }
 
 ProfStat Model::profile_read(int cat) {

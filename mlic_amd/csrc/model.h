@@ -28,6 +28,7 @@ struct ConvW {
   _Float16* wh = nullptr;    // split hi/lo [Cout][K*K][cin_pad]  (f16x3 MFMA path)
   _Float16* wl = nullptr;
   int cin_pad = 0;
+  std::string name;          // state_dict prefix (profiling)
 };
 
 enum Precision : int { PREC_F32 = 0, PREC_F16X3 = 1 };
@@ -93,6 +94,7 @@ struct Lane {
     hipEvent_t a, b;
     int cat;
     double flops, bytes;
+    std::string tag;
   };
   bool prof = false;
   std::vector<ProfRec> recs;
@@ -128,6 +130,7 @@ class Model {
   int precision() const { return precision_; }
   int lanes() const { return nlanes_; }
   ProfStat profile_read(int cat);  // synchronises the recorded events; clears that category
+  std::string profile_layers();     // per-tag table of the recorded events (does not clear)
   size_t weight_bytes() const { return wbytes_; }
   // module-level entry points for tests
   void run_module(const std::string& which, int idx, const float* in0, const float* in1, int B, int Cin, int H, int W,
@@ -154,7 +157,7 @@ class Model {
   Lane& lane(int i);
   hipEvent_t next_event();
   template <class F>
-  void timed(int cat, double flops, double bytes, F&& launch);
+  void timed(int cat, double flops, double bytes, F&& launch, const std::string& tag = std::string());
   // run fn(lane, first_image, count) over the batch split across lanes (host threads)
   template <class F>
   void over_lanes(int B, hipStream_t caller, F&& fn);
