@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 CONV32 = ["conv_mfma_kernel<64,64>", "conv_mfma_kernel<64,128>", "conv_mfma_kernel<128,64>",
           "conv_mfma_kernel<128,128>"]
-CONVX3 = ["conv_f16x3_kernel<64,64>", "conv_f16x3_kernel<64,128>", "conv_f16x3_kernel<128,64>",
+CONVX3 = ["conv_f16x3_kernel<32,256>", "conv_f16x3_kernel<64,128>", "conv_f16x3_kernel<128,64>",
           "conv_f16x3_kernel<128,128>"]
 CATS = CONV32 + CONVX3 + ["dw3x3_kernel", "local_attn_kernel", "linear_attention", "elementwise"]
 # dense peak of the arithmetic each conv kernel runs on (MI355X_MICROARCH.md): fp32 MFMA 157.3 TF;

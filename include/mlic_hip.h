@@ -71,7 +71,7 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
  * noise), 0 = fp32 MFMA.  Also $MLIC_PRECISION. */
 int mlic_set_precision(mlic_model* m, int precision);
 /* live kernel timing (HIP events on the executor stream): categories 0..3 conv_mfma_kernel (fp32)
- * <64,64>, <64,128>, <128,64>, <128,128>; 4..7 conv_f16x3_kernel with the same tiles; 8 depthwise;
+ * <64,64>, <64,128>, <128,64>, <128,128>; 4..7 conv_f16x3_kernel <32,256>, <64,128>, <128,64>, <128,128>; 8 depthwise;
  * 9 local attention; 10 linear attention; 11 elementwise/reductions.  read() sums and clears. */
 int mlic_set_profiling(mlic_model* m, int on);
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes);
@@ -79,7 +79,9 @@ int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, dou
  * conv events, sorted by time; call before mlic_profile_read (which clears) */
 int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written);
 
-/* kernel-level entry points (bit-exact tests) */
+/* kernel-level entry points (bit-exact tests, micro-benchmarks) */
+int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
+                    double* ms_per, double* tflops);
 int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */
 int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);
 int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out);

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "model.h"
 
@@ -181,6 +182,66 @@ int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written) {
       std::memcpy(buf, s.data(), n);
       buf[n] = 0;
     }
+  });
+}
+
+// conv micro-benchmark: random operands of one layer shape, `iters` launches timed with events.
+// impl: 0 = conv_mfma (fp32), 1 = conv_f16x3.  Returns ms per launch and TFLOP/s (algorithmic).
+int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
+                    double* ms_per, double* tflops) {
+  return guard([&] {
+    const int pad = K / 2;
+    const int Ho = (H + 2 * pad - K) / stride + 1, Wo = (W + 2 * pad - K) / stride + 1;
+    const int64_t nx = (int64_t)B * Cin * H * W, ny = (int64_t)B * Cout * Ho * Wo, nw = (int64_t)Cout * Cin * K * K;
+    const int cin_pad = (Cin + 31) / 32 * 32;
+    const int64_t nh = (int64_t)Cout * K * K * cin_pad;
+    float *x, *y, *w, *wp, *bias;
+    _Float16 *wh, *wl;
+    HIP_OK(hipMalloc(&x, nx * 4));
+    HIP_OK(hipMalloc(&y, ny * 4));
+    HIP_OK(hipMalloc(&w, nw * 4));
+    HIP_OK(hipMalloc(&wp, nw * 4));
+    HIP_OK(hipMalloc(&bias, Cout * 4));
+    HIP_OK(hipMalloc(&wh, nh * 2));
+    HIP_OK(hipMalloc(&wl, nh * 2));
+    {
+      std::vector<float> hx(std::max(nx, nw));
+      uint32_t st = 12345;
+      for (auto& v : hx) { st = st * 1664525u + 1013904223u; v = ((st >> 9) * (1.0f / 8388608.0f)) - 0.5f; }
+      HIP_OK(hipMemcpy(x, hx.data(), nx * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(w, hx.data(), nw * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMemset(bias, 0, Cout * 4));
+    }
+    pack_conv(w, wp, Cout, Cin, K * K, nullptr);
+    split_weights(w, wh, wl, Cout, Cin, K * K, cin_pad, nullptr);
+    ConvParams P{};
+    P.nseg = 1;
+    P.seg[0] = {x, Cin, (int64_t)Cin * H * W};
+    P.Cin = Cin; P.H = H; P.W = W; P.Cout = Cout; P.Ho = Ho; P.Wo = Wo; P.K = K; P.stride = stride; P.pad = pad;
+    P.wpk = wp; P.bias = bias; P.out = y; P.B = B;
+    P.out_bs = (int64_t)Cout * Ho * Wo;
+    P.out_cs = (int64_t)Ho * Wo;
+    P.epi = shuffle ? EPI_SHUFFLE : 0;
+    auto launch = [&] {
+      if (impl == 1) conv_f16x3_forward(P, wh, wl, cin_pad, nullptr);
+      else conv_forward(P, nullptr);
+    };
+    launch();
+    HIP_OK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    HIP_OK(hipEventCreate(&a));
+    HIP_OK(hipEventCreate(&b));
+    HIP_OK(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i) launch();
+    HIP_OK(hipEventRecord(b, nullptr));
+    HIP_OK(hipEventSynchronize(b));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, a, b));
+    *ms_per = ms / iters;
+    *tflops = 2.0 * (double)B * Cout * Ho * Wo * Cin * K * K / (*ms_per * 1e-3) / 1e12;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl}) (void)hipFree(p);
   });
 }
 

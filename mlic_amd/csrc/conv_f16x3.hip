@@ -24,12 +24,13 @@ constexpr int XB_K = 32;         // k per tile
 constexpr int XB_PITCH = 40;     // halves per LDS row (32 + 8 pad) = 80 bytes
 constexpr int XB_THREADS = 256;
 
-template <int BM, int BN>
+template <int BM, int BN, int WAVES_M = 2>
 __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, const _Float16* __restrict__ wh,
                                                                  const _Float16* __restrict__ wl, int cin_pad) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_CHUNKS = BM * XB_K / 8 / XB_THREADS;  // 16-byte chunks per thread per operand half
+  constexpr int A_CHUNKS = (BM * XB_K / 8 + XB_THREADS - 1) / XB_THREADS;  // 16-byte chunks per thread
   constexpr int B_ROWS = XB_K * BN / XB_THREADS;         // fp32 values staged per thread
   constexpr int G = B_ROWS < 16 ? B_ROWS : 16;          // channels per segment-uniform group
   static_assert(A_CHUNKS >= 1 && (B_ROWS == 8 || B_ROWS == 16 || B_ROWS == 32), "tile");
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
 
   const int nct = gridDim.x, npt = gridDim.y, nblk = nct * npt;
   const int bid = blockIdx.y * nct + blockIdx.x;
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
       const int id = tid + i * XB_THREADS;
       const int row = id >> 2, q = id & 3;
       const int co = co0 + row;
-      if (co < P.Cout) {
+      if (row < BM && co < P.Cout) {
         const int64_t off = ((int64_t)co * KK + tap) * cin_pad + c0 + 8 * q;
         ra_h[i] = *reinterpret_cast<const uint4*>(wh + off);
         ra_l[i] = *reinterpret_cast<const uint4*>(wl + off);
@@ -118,6 +119,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
     for (int i = 0; i < A_CHUNKS; ++i) {
       const int id = tid + i * XB_THREADS;
       const int row = id >> 2, q = id & 3;
+      if (row >= BM) continue;
       *reinterpret_cast<uint4*>(base + row * XB_PITCH + 8 * q) = ra_h[i];
       *reinterpret_cast<uint4*>(base + A_SZ + row * XB_PITCH + 8 * q) = ra_l[i];
     }
@@ -225,15 +227,16 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
 
 int conv_f16x3_variant(const ConvParams& P) {
   const int64_t HWo = (int64_t)P.Ho * P.Wo;
-  if (P.Cout <= 64) return HWo >= 128 * 256 ? 1 : 0;
+  if (P.Cout <= 32) return 0;  // <32,256>, waves 1x4 (small-Cout heads, e.g. g_s's 192->12)
+  if (P.Cout <= 64) return 1;  // <64,128>
   return HWo >= 128 * 512 ? 3 : 2;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WAVES_M = 2>
 static void launch_x3(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   const int HWo = P.Ho * P.Wo;
   dim3 grid((P.Cout + BM - 1) / BM, (HWo + BN - 1) / BN, P.B);
-  hipLaunchKernelGGL((conv_f16x3_kernel<BM, BN>), grid, dim3(XB_THREADS), 0, st, P, wh, wl, cin_pad);
+  hipLaunchKernelGGL((conv_f16x3_kernel<BM, BN, WAVES_M>), grid, dim3(XB_THREADS), 0, st, P, wh, wl, cin_pad);
   HIP_OK(hipGetLastError());
 }
 
@@ -242,7 +245,7 @@ void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16*
   MLIC_CHECK(cin_pad % XB_K == 0 && cin_pad >= P.Cin, "f16x3: padded Cin");
   for (int s = 0; s + 1 < P.nseg; ++s) MLIC_CHECK(P.seg[s].C % 16 == 0, "f16x3: segments must be 16-aligned");
   switch (conv_f16x3_variant(P)) {
-    case 0: launch_x3<64, 64>(P, wh, wl, cin_pad, st); break;
+    case 0: launch_x3<32, 256, 1>(P, wh, wl, cin_pad, st); break;
     case 1: launch_x3<64, 128>(P, wh, wl, cin_pad, st); break;
     case 2: launch_x3<128, 64>(P, wh, wl, cin_pad, st); break;
     default: launch_x3<128, 128>(P, wh, wl, cin_pad, st); break;

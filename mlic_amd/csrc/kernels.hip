@@ -18,26 +18,31 @@
 namespace mlic {
 
 // =============================================================================================
-// depthwise 3x3, pad 1
-constexpr int DW_TW = 64, DW_TH = 8;
+// depthwise 3x3, pad 1.  One workgroup = one (image, channel) plane tile; the input tile with its
+// halo is staged in LDS with coalesced row loads, and each thread produces a 4-wide strip of
+// outputs (float4 store) from a 3 x (4*s + 2) register window, so every staged value is reused.
+constexpr int DW_TW = 128;  // output tile width
+constexpr int DW_TH1 = 32;  // output tile height, stride 1
+constexpr int DW_TH2 = 16;  // output tile height, stride 2
 
+template <int S>
 __global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
-  __shared__ float tile[(DW_TH * 2 + 2) * (DW_TW * 2 + 2)];
-  const int s = P.stride;
-  const int tw_in = DW_TW * s + 2, th_in = DW_TH * s + 2;
+  constexpr int TH = S == 1 ? DW_TH1 : DW_TH2;
+  constexpr int TWI = DW_TW * S + 2, THI = TH * S + 2;
+  constexpr int PITCH = TWI + 1;
+  __shared__ float tile[THI * PITCH];
   const int c = blockIdx.y, b = blockIdx.z;
   const int ntx = (P.Wo + DW_TW - 1) / DW_TW;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int ox0 = tx * DW_TW, oy0 = ty * DW_TH;
-  const int ix0 = ox0 * s - 1, iy0 = oy0 * s - 1;
-  // segment lookup
+  const int ox0 = tx * DW_TW, oy0 = ty * TH;
+  const int ix0 = ox0 * S - 1, iy0 = oy0 * S - 1;
   int sg = 0, c0 = 0;
   while (sg + 1 < P.nseg && c >= c0 + P.seg[sg].C) { c0 += P.seg[sg].C; ++sg; }
   const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
-  for (int i = threadIdx.x; i < tw_in * th_in; i += 256) {
-    const int yy = i / tw_in, xx = i - yy * tw_in;
+  for (int i = threadIdx.x; i < TWI * THI; i += 256) {
+    const int yy = i / TWI, xx = i - yy * TWI;
     const int gy = iy0 + yy, gx = ix0 + xx;
-    tile[i] = (gy >= 0 && gy < P.H && gx >= 0 && gx < P.W) ? src[(int64_t)gy * P.W + gx] : 0.0f;
+    tile[yy * PITCH + xx] = (gy >= 0 && gy < P.H && gx >= 0 && gx < P.W) ? src[(int64_t)gy * P.W + gx] : 0.0f;
   }
   __syncthreads();
   float w[9];
@@ -45,19 +50,38 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
   for (int k = 0; k < 9; ++k) w[k] = P.w[c * 9 + k];
   const float bias = P.bias ? P.bias[c] : 0.0f;
   float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)c * P.Ho * P.Wo;
-  for (int i = threadIdx.x; i < DW_TW * DW_TH; i += 256) {
-    const int ly = i / DW_TW, lx = i - ly * DW_TW;
-    const int oy = oy0 + ly, ox = ox0 + lx;
-    if (oy >= P.Ho || ox >= P.Wo) continue;
-    const float* t = tile + (ly * s) * tw_in + lx * s;
-    float acc = 0.0f;
+  const bool vec = (P.Wo & 3) == 0;
+  // 32 strips of 4 outputs per row; 256 threads cover 8 rows per pass
+  const int xs = (threadIdx.x & 31) * 4;
+  for (int ly = threadIdx.x >> 5; ly < TH; ly += 8) {
+    const int oy = oy0 + ly;
+    if (oy >= P.Ho) break;
+    float win[3][4 * S + 2];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], t[ky * tw_in + kx], acc);
-    float v = acc + bias;
-    if (P.gelu) v = gelu_erf(v);
-    dst[(int64_t)oy * P.Wo + ox] = v;
+      for (int j = 0; j < 4 * S + 2; ++j) win[ky][j] = tile[(ly * S + ky) * PITCH + xs * S + j];
+    float o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], win[ky][q * S + kx], acc);
+      float v = acc + bias;
+      if (P.gelu) v = gelu_erf(v);
+      o[q] = v;
+    }
+    const int ox = ox0 + xs;
+    float* d = dst + (int64_t)oy * P.Wo + ox;
+    if (vec && ox + 3 < P.Wo) {
+      *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ox + q < P.Wo) d[q] = o[q];
+    }
   }
 }
 
@@ -67,8 +91,10 @@ void dw3x3(const DwParams& P, hipStream_t st) {
   int tot = 0;
   for (int i = 0; i < P.nseg; ++i) tot += P.seg[i].C;
   MLIC_CHECK(tot == P.C, "dw segments");
-  const int ntx = (P.Wo + DW_TW - 1) / DW_TW, nty = (P.Ho + DW_TH - 1) / DW_TH;
-  hipLaunchKernelGGL(dw3x3_kernel, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
+  const int TH = P.stride == 1 ? DW_TH1 : DW_TH2;
+  const int ntx = (P.Wo + DW_TW - 1) / DW_TW, nty = (P.Ho + TH - 1) / TH;
+  if (P.stride == 1) hipLaunchKernelGGL(dw3x3_kernel<1>, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
+  else hipLaunchKernelGGL(dw3x3_kernel<2>, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
   HIP_OK(hipGetLastError());
 }
 
