@@ -149,7 +149,7 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
 
 int mlic_set_precision(mlic_model* m, int precision) {
   return guard([&] {
-    MLIC_CHECK(precision == PREC_F32 || precision == PREC_F16X3, "precision must be 0 (f32) or 1 (f16x3)");
+    MLIC_CHECK(precision >= PREC_F32 && precision <= PREC_F16X3_V2, "precision must be 0 (f32), 1 or 2 (f16x3)");
     m->impl->set_precision(precision);
   });
 }
@@ -224,6 +224,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     P.epi = shuffle ? EPI_SHUFFLE : 0;
     auto launch = [&] {
       if (impl == 1) conv_f16x3_forward(P, wh, wl, cin_pad, nullptr);
+      else if (impl == 2) conv_x3v2_forward(P, wh, wl, cin_pad, nullptr);
       else conv_forward(P, nullptr);
     };
     launch();

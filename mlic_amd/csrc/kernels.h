@@ -13,6 +13,8 @@ void conv_forward(const ConvParams& P, hipStream_t st);
 // hi/lo fp16 [Cout][K*K][cin_pad] (cin_pad = Cin rounded up to 32)
 int conv_f16x3_variant(const ConvParams& P);
 void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
+int conv_x3v2_variant(const ConvParams& P);
+void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad,
                    hipStream_t st);
 

@@ -299,7 +299,10 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
   const double outn = (double)L().B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * cin * w.K * w.K;
   const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  if (precision_ == PREC_F16X3 && w.wh) {
+  if (precision_ == PREC_F16X3_V2 && w.wh) {
+    timed(PROF_CONVX3 + conv_x3v2_variant(P), flops, bytes,
+          [&] { conv_x3v2_forward(P, w.wh, w.wl, w.cin_pad, L().st); }, w.name);
+  } else if (precision_ == PREC_F16X3 && w.wh) {
     timed(PROF_CONVX3 + conv_f16x3_variant(P), flops, bytes,
           [&] { conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, L().st); }, w.name);
   } else {

@@ -31,7 +31,7 @@ struct ConvW {
   std::string name;          // state_dict prefix (profiling)
 };
 
-enum Precision : int { PREC_F32 = 0, PREC_F16X3 = 1 };
+enum Precision : int { PREC_F32 = 0, PREC_F16X3 = 1, PREC_F16X3_V2 = 2 };
 struct DwW {
   const float* w = nullptr;  // [C][9]
   const float* b = nullptr;

@@ -19,9 +19,12 @@ SHAPES = [
 ]
 
 
+EXTRA = [("g_s.7 subpel 3x3 192->12 @544x960", 8, 192, 12, 544, 960, 3, 1, 1)]
+
+
 def main():
     impls = [int(a) for a in sys.argv[1:]] or [0, 1]
-    for name, B, Cin, Cout, H, W, K, s, sh in SHAPES:
+    for name, B, Cin, Cout, H, W, K, s, sh in SHAPES + EXTRA:
         row = [f"{name:40s}"]
         for impl in impls:
             ms, tf = C.c_double(), C.c_double()
