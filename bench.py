@@ -112,6 +112,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from mlic_amd import _lib, get_model, synthetic
+    from mlic_amd import dist as mdist
     net = get_model(a.model)
     net.load_state_dict(synthetic.synth_state_dict(a.model, 0))
     net = net.to(dev).eval()
@@ -145,18 +146,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # per-image records {bytes, bpp_file, psnr}: the one collective (all_gather, RCCL over xGMI)
-    rec = torch.zeros(B, 3, dtype=torch.float64, device=dev)
+    # per-image records: the one collective (all_gather over RCCL/xGMI), mlic_amd.dist
+    F = {k: i for i, k in enumerate(mdist.RECORD_FIELDS)}
+    rec = torch.zeros(B, mdist.RECORD_LEN, dtype=torch.float64)
     for i in range(B):
         nbytes = len(c["strings"][0][i]) + len(c["strings"][1][i])
-        rec[i, 0] = nbytes
-        rec[i, 1] = 8.0 * nbytes / (H * W)
-        rec[i, 2] = psnr_u8(x[i], d["x_hat"][i])
-    if distributed:
-        allrec = [torch.zeros_like(rec) for _ in range(world)]
-        dist.all_gather(allrec, rec)
-        rec = torch.cat(allrec)
-    rec = rec.cpu()
+        rec[i, F["job"]] = rank * B + i
+        rec[i, F["H"]], rec[i, F["W"]] = H, W
+        rec[i, F["bytes"]] = nbytes
+        rec[i, F["bpp_file"]] = 8.0 * nbytes / (H * W)
+        rec[i, F["psnr"]] = psnr_u8(x[i], d["x_hat"][i])
+    rec = mdist.gather_records(rec.to(dev), max_per_rank=B).cpu()
+    rec = rec[:, [F["bytes"], F["bpp_file"], F["psnr"]]]
 
     # live roofline of the dominant kernel family: one extra profiled (untimed) step
     h = net._handle

@@ -1,0 +1,62 @@
+"""Multi-process (gloo, world_size 2) checks of the image sharding and record gather."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mlic_amd import dist as mdist
+
+
+def test_lpt_shard_balances_and_covers():
+    sizes = [(2176, 3840)] * 2 + [(1088, 1920)] * 6 + [(512, 768)] * 8
+    shards = mdist.lpt_shard(sizes, 4)
+    assert sorted(i for s in shards for i in s) == list(range(len(sizes)))
+    loads = [sum(mdist.padded_pixels(*sizes[i]) for i in s) for s in shards]
+    assert max(loads) - min(loads) <= mdist.padded_pixels(1088, 1920)
+    assert mdist.lpt_shard(sizes, 4) == shards  # deterministic
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, njobs, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sizes = [(64 * (1 + j % 3), 64 * (2 + j % 2)) for j in range(njobs)]
+    mine = mdist.lpt_shard(sizes, world)[rank]
+    rec = torch.zeros(len(mine), mdist.RECORD_LEN, dtype=torch.float64)
+    for k, j in enumerate(mine):
+        rec[k, 0] = j
+        rec[k, 1], rec[k, 2] = sizes[j]
+        rec[k, 8] = 30.0 + j  # "psnr"
+    allrec = mdist.gather_records(rec, max_per_rank=njobs)
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing
+    if rank == 0:
+        q.put((allrec.tolist(), float(t)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_records_world2():
+    world, njobs = 2, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, njobs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rows, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert tmax == 2.0
+    assert [int(r[0]) for r in rows] == list(range(njobs))
+    assert all(abs(r[8] - (30.0 + r[0])) < 1e-9 for r in rows)
