@@ -29,14 +29,21 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-CONV32 = ["conv_mfma_kernel<64,64>", "conv_mfma_kernel<64,128>", "conv_mfma_kernel<128,64>",
-          "conv_mfma_kernel<128,128>"]
-CONVX3 = ["conv_f16x3_kernel<32,256>", "conv_f16x3_kernel<64,128>", "conv_f16x3_kernel<128,64>",
-          "conv_f16x3_kernel<128,128>"]
-CATS = CONV32 + CONVX3 + ["dw3x3_kernel", "local_attn_kernel", "linear_attention", "elementwise"]
-# dense peak of the arithmetic each conv kernel runs on (MI355X_MICROARCH.md): fp32 MFMA 157.3 TF;
-# f16x3 issues 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of fp32-equivalent work
-PEAK = {**{k: 157.3 for k in CONV32}, **{k: 2500.0 / 3 for k in CONVX3}}
+# dense peak of the arithmetic each kernel family runs on (MI355X_MICROARCH.md): fp32 MFMA 157.3 TF;
+# the split-fp16 kernels issue 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of
+# fp32-equivalent work; the VALU conv kernels run exact fp32 FMAs (157.3 TF with packed FMA)
+def kernel_peak(name: str):
+    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident")):
+        return 2500.0 / 3, "3 x v_mfma_f32_32x32x16_f16 per fp32 product (split-fp16)"
+    if name.startswith("conv_mfma"):
+        return 157.3, "v_mfma_f32_32x32x2_f32"
+    return 157.3, "fp32 VALU FMA"
+
+
+def is_conv(name: str) -> bool:
+    return name.startswith(("conv", "pw_resident"))
+
+
 METRIC = "images/sec (enc+dec) at 1920×1088 MLICPP_L, 1/2/4/8 GPU; bpp/PSNR Δ vs ref"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense, exact f32)
 PEAK_HBM_GBS = 8000.0
@@ -53,8 +60,9 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("MLIC_LANES", "4")),
                     help="host threads x HIP streams per GPU for compress/decompress")
-    ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "1")),
-                    help="dense-conv arithmetic: 1 = split-fp16 MFMA (f16x3), 0 = fp32 MFMA")
+    ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "2")),
+                    help="dense-conv arithmetic: 2 = split-fp16 MFMA v2 + specialised kernels, "
+                         "1 = f16x3 v1 tiles, 0 = fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers-out", default="", help="write the per-layer conv timing table here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -176,20 +184,34 @@ def main():
             with open(a.layers_out, "w") as f:
                 f.write(buf.value.decode())
     fam = {}
-    for cat, nm in enumerate(CATS):
+    ncat = C.c_int()
+    _lib.call("mlic_profile_categories", C.byref(ncat))
+    for cat in range(ncat.value):
+        nb = C.create_string_buffer(128)
+        _lib.call("mlic_profile_category_name", cat, nb, 128)
         n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
         _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
-        fam[nm] = {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
-    # dominant kernel = the conv tile instantiation with the most device time
-    dom = max(CONV32 + CONVX3, key=lambda k: fam[k]["ms"])
+        fam[nb.value.decode()] = {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
+    # dominant kernel = the conv kernel instantiation with the most device time; its roofline bound
+    # is whichever ceiling is lower at its arithmetic intensity (algorithmic FLOPs / bytes)
+    convs = [k for k in fam if is_conv(k)]
+    dom = max(convs, key=lambda k: fam[k]["ms"])
     conv = fam[dom]
-    achieved = conv["flops"] / (conv["ms"] * 1e-3) / 1e12 if conv["ms"] > 0 else 0.0
-    conv_all = {k: sum(fam[c][k] for c in CONV32 + CONVX3) for k in ("launches", "ms", "flops")}
+    peak_tf, arith = kernel_peak(dom)
+    sec = max(conv["ms"], 1e-9) * 1e-3
+    ai = conv["flops"] / max(conv["bytes"], 1.0)
+    hbm_bound = ai * PEAK_HBM_GBS * 1e9 < peak_tf * 1e12
+    if hbm_bound:
+        bound, unit, achieved, peak = "hbm", "GB/s", conv["bytes"] / sec / 1e9, PEAK_HBM_GBS
+    else:
+        bound, unit, achieved, peak = "mfma", "TFLOP/s", conv["flops"] / sec / 1e12, peak_tf
+    conv_all = {k: sum(fam[c][k] for c in convs) for k in ("launches", "ms", "flops")}
     traffic = None
     try:
         with open(a.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("model") == a.model and tj.get("H") == H and tj.get("W") == W:
+        if (tj.get("model") == a.model and tj.get("H") == H and tj.get("W") == W
+                and tj.get("kernel", "") and tj["kernel"] in dom):
             traffic = tj.get("conv_hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -213,17 +235,16 @@ def main():
             "config": {"workload": f"{a.model} compress+decompress (full rANS bitstreams) of {W}x{H} images",
                        "model": a.model, "global_batch": B * world, "per_gpu_batch": B, "H": H, "W": W,
                        "parallelism": f"image-sharded x{world} (no cross-GPU context)"},
-            "roofline": {"bound": "mfma", "kernel": dom + (" (implicit-GEMM conv, 3 x v_mfma_f32_32x32x16_f16 split-fp16)"
-                                                           if "f16x3" in dom else
-                                                           " (implicit-GEMM conv, v_mfma_f32_32x32x2_f32)"),
-                         "achieved": round(achieved, 3), "peak": round(PEAK[dom], 1), "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK[dom], 4),
+            "roofline": {"bound": bound, "kernel": f"{dom} ({arith})",
+                         "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
+                         "frac": round(achieved / peak, 4),
                          "traffic": traffic,
                          "launches_per_step": conv["launches"],
                          "avg_launch_us": round(1000 * conv["ms"] / max(1, conv["launches"]), 2),
                          "algorithmic_flops_per_launch": round(conv["flops"] / max(1, conv["launches"])),
+                         "algorithmic_bytes_per_launch": round(conv["bytes"] / max(1, conv["launches"])),
                          "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3)},
-            "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items()},
+            "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
             "quality": {"bpp_file_mean": round(float(rec[:, 1].mean()), 5),
                         "psnr_u8_mean": round(float(rec[:, 2].mean()), 4), "images": int(rec.shape[0])},

@@ -67,19 +67,29 @@ int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, con
                     int B, int Cin, int H, int W, float* out);
 int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
 
-/* dense-conv arithmetic: 1 = split-fp16 MFMA "f16x3" (default; error below fp32 summation-order
- * noise), 0 = fp32 MFMA.  Also $MLIC_PRECISION. */
+/* dense-conv arithmetic: 2 = split-fp16 MFMA "f16x3" v2 tiles + specialised kernels (default; error
+ * below fp32 summation-order noise), 1 = f16x3 v1 tiles, 0 = fp32 MFMA.  Also $MLIC_PRECISION. */
 int mlic_set_precision(mlic_model* m, int precision);
-/* live kernel timing (HIP events on the executor stream): categories 0..3 conv_mfma_kernel (fp32)
- * <64,64>, <64,128>, <128,64>, <128,128>; 4..7 conv_f16x3_kernel <32,256>, <64,128>, <128,64>, <128,128>; 8 depthwise;
- * 9 local attention; 10 linear attention; 11 elementwise/reductions.  read() sums and clears. */
+/* live kernel timing (HIP events on the executor stream), one category per kernel family / tile
+ * instantiation: mlic_profile_categories gives the count, mlic_profile_category_name the kernel
+ * name of each.  read() sums and clears. */
 int mlic_set_profiling(mlic_model* m, int on);
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes);
 /* tab-separated per-layer table (layer, category, launches, ms, GFLOP, TFLOP/s) of the recorded
  * conv events, sorted by time; call before mlic_profile_read (which clears) */
 int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written);
 
+int mlic_profile_categories(int* n);
+int mlic_profile_category_name(int cat, char* buf, size_t cap);
+
 /* kernel-level entry points (bit-exact tests, micro-benchmarks) */
+/* one conv layer with a given kernel family: impl -1 = the model's choice (precision 2), 0 fp32 MFMA,
+ * 1 f16x3, 2 f16x3 v2, 3 resident-weight 1x1, 4 narrow 3x3, 5 small-Cin 1x1.  w is torch layout
+ * [Cout][Cin][K][K]; pad = K/2; epi = Epi flags of common.h (aux for GDN, res for residual).
+ * Synchronous on `stream`. */
+int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,
+                  int Cout, int H, int W, int K, int stride, int epi, const float* aux, const float* res);
+/* impl 0..2 as mlic_conv_run, 3 = the model's choice */
 int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
                     double* ms_per, double* tflops);
 int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */

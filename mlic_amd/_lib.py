@@ -44,6 +44,9 @@ def _sig(lib):
         "mlic_profile_layers": [p, p, sz, P(sz)],
         "mlic_bench_conv": [i, i, i, i, i, i, i, i, i, i, P(C.c_double), P(C.c_double)],
         "mlic_profile_read": [p, i, P(i64), P(C.c_double), P(C.c_double), P(C.c_double)],
+        "mlic_profile_categories": [P(i)],
+        "mlic_profile_category_name": [i, p, sz],
+        "mlic_conv_run": [p, i, p, p, p, p, i, i, i, i, i, i, i, i, p, p],
         "mlic_image_sq_err_u8": [p, p, p, i, i64, p],
         "mlic_neglog2_sum": [p, p, i, i64, p],
         "mlic_pmf_to_quantized_cdf": [p, i, i, p],

@@ -164,7 +164,7 @@ int mlic_set_profiling(mlic_model* m, int on) {
 
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes) {
   return guard([&] {
-    MLIC_CHECK(cat >= 0 && cat < PROF_NCAT, "profile category");
+    MLIC_CHECK(cat >= 0 && cat < PCAT_COUNT, "profile category");
     ProfStat s = m->impl->profile_read(cat);
     *launches = s.launches;
     *ms = s.ms;
@@ -222,11 +222,9 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     P.out_bs = (int64_t)Cout * Ho * Wo;
     P.out_cs = (int64_t)Ho * Wo;
     P.epi = shuffle ? EPI_SHUFFLE : 0;
-    auto launch = [&] {
-      if (impl == 1) conv_f16x3_forward(P, wh, wl, cin_pad, nullptr);
-      else if (impl == 2) conv_x3v2_forward(P, wh, wl, cin_pad, nullptr);
-      else conv_forward(P, nullptr);
-    };
+    const ConvWeights cw{wp, wh, wl, cin_pad};
+    const int which = impl == 3 ? conv_select(P, cw, 2) : impl;  // 3 = what the model runs (precision 2)
+    auto launch = [&] { conv_run(which, P, cw, nullptr); };
     launch();
     HIP_OK(hipDeviceSynchronize());
     hipEvent_t a, b;
@@ -243,6 +241,60 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl}) (void)hipFree(p);
+  });
+}
+
+int mlic_profile_categories(int* n) {
+  return guard([&] { *n = PCAT_COUNT; });
+}
+
+int mlic_profile_category_name(int cat, char* buf, size_t cap) {
+  return guard([&] {
+    MLIC_CHECK(cat >= 0 && cat < PCAT_COUNT, "profile category");
+    const std::string nm = prof_cat_name(cat);
+    MLIC_CHECK(cap > nm.size(), "buffer too small");
+    std::memcpy(buf, nm.c_str(), nm.size() + 1);
+  });
+}
+
+int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,
+                  int Cout, int H, int W, int K, int stride, int epi, const float* aux, const float* res) {
+  return guard([&] {
+    hipStream_t st = (hipStream_t)stream;
+    const int pad = K / 2;
+    const int Ho = (H + 2 * pad - K) / stride + 1, Wo = (W + 2 * pad - K) / stride + 1;
+    const int cin_pad = (Cin + 31) / 32 * 32;
+    const int64_t nw = (int64_t)Cout * Cin * K * K, nh = (int64_t)Cout * K * K * cin_pad;
+    float* wp = nullptr;
+    _Float16 *wh = nullptr, *wl = nullptr;
+    HIP_OK(hipMallocAsync((void**)&wp, nw * 4, st));
+    HIP_OK(hipMallocAsync((void**)&wh, nh * 2, st));
+    HIP_OK(hipMallocAsync((void**)&wl, nh * 2, st));
+    pack_conv(w, wp, Cout, Cin, K * K, st);
+    split_weights(w, wh, wl, Cout, Cin, K * K, cin_pad, st);
+    ConvParams P{};
+    P.nseg = 1;
+    P.seg[0] = {x, Cin, (int64_t)Cin * H * W};
+    P.Cin = Cin; P.H = H; P.W = W; P.Cout = Cout; P.Ho = Ho; P.Wo = Wo; P.K = K; P.stride = stride; P.pad = pad;
+    P.wpk = wp; P.bias = bias; P.out = y; P.B = B; P.epi = epi;
+    const bool shuffle = (epi & EPI_SHUFFLE) != 0;
+    MLIC_CHECK(!shuffle || Cout % 4 == 0, "shuffle needs Cout % 4 == 0");
+    P.out_cs = shuffle ? (int64_t)4 * Ho * Wo : (int64_t)Ho * Wo;
+    P.out_bs = (int64_t)Cout * Ho * Wo;
+    MLIC_CHECK(!(epi & (EPI_GDN | EPI_IGDN)) || aux, "GDN epilogue needs aux");
+    MLIC_CHECK(!(epi & EPI_RES) || res, "residual epilogue needs res");
+    P.aux = aux; P.aux_bs = (int64_t)Cout * Ho * Wo;
+    P.res = res; P.res_bs = P.out_bs;
+    const ConvWeights cw{wp, wh, wl, cin_pad};
+    const int which = impl < 0 ? conv_select(P, cw, 2) : impl;
+    if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
+    if (which == CONV_NARROW) MLIC_CHECK(conv_narrow_ok(P), "narrow: unsupported shape");
+    if (which == CONV_SMALLCIN) MLIC_CHECK(conv_smallcin_ok(P), "smallcin: unsupported shape");
+    conv_run(which, P, cw, st);
+    HIP_OK(hipFreeAsync(wp, st));
+    HIP_OK(hipFreeAsync(wh, st));
+    HIP_OK(hipFreeAsync(wl, st));
+    HIP_OK(hipStreamSynchronize(st));
   });
 }
 

@@ -95,4 +95,35 @@ __device__ __forceinline__ float gelu_erf(float x) {
 
 __device__ __forceinline__ bool is_anchor(int h, int w) { return ((h + w) & 1) == 1; }
 
+// the shared conv epilogue: bias, activation/normalisation, masks, residual, (shuffled) store of
+// output channel co at conv-grid pixel p of image b (flag order as the Epi enum)
+__device__ __forceinline__ void conv_store(const ConvParams& P, int b, int co, int p, float v) {
+  const int epi = P.epi;
+  const int HWo = P.Ho * P.Wo;
+  if (P.bias) v += P.bias[co];
+  if (epi & EPI_GELU) v = gelu_erf(v);
+  if (epi & (EPI_GDN | EPI_IGDN)) {
+    const float x = P.aux[(int64_t)b * P.aux_bs + (int64_t)co * HWo + p];
+    v = (epi & EPI_GDN) ? x * (1.0f / sqrtf(v)) : x * sqrtf(v);
+  }
+  if (epi & EPI_TANH_HALF) v = 0.5f * tanhf(v);
+  int oh = 0, ow = 0;
+  if (epi & (EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR | EPI_SHUFFLE)) {
+    oh = p / P.Wo;
+    ow = p - oh * P.Wo;
+  }
+  if (epi & EPI_MASK_ANCHOR) v = is_anchor(oh, ow) ? v : 0.0f;
+  if (epi & EPI_MASK_NONANCHOR) v = is_anchor(oh, ow) ? 0.0f : v;
+  int64_t off;
+  if (epi & EPI_SHUFFLE) {
+    const int oc = co >> 2;
+    const int y2 = 2 * oh + ((co >> 1) & 1), x2 = 2 * ow + (co & 1);
+    off = (int64_t)oc * P.out_cs + (int64_t)y2 * (2 * P.Wo) + x2;
+  } else {
+    off = (int64_t)co * P.out_cs + p;
+  }
+  if (epi & EPI_RES) v = P.res[(int64_t)b * P.res_bs + off] + v;
+  P.out[(int64_t)b * P.out_bs + off] = v;
+}
+
 }  // namespace mlic

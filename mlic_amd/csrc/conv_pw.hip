@@ -1,0 +1,439 @@
+// Specialised convolution kernels for the shapes the generic implicit-GEMM tiles handle badly.
+//
+// 1. pw_resident_kernel — 1x1 stride-1 convs whose split weight matrix fits in LDS (Cin = Cout = N
+//    of g_a / g_s: the dwsep point convs and GDN/IGDN at full and half resolution, K = 96..192).
+//    With K = 192 a tiled GEMM spends most of its time in prologue/epilogue latency (6 K-tiles per
+//    block).  Here each CU keeps the whole hi/lo weight matrix resident in LDS for the life of the
+//    block (loaded once), and each of its 8 waves streams its own 32-pixel columns: the B fragments
+//    of v_mfma_f32_32x32x16_f16 (lane l: pixel l&31, channels 8(l>>5)..+7 of each 16-deep k-step)
+//    come straight from HBM into VGPRs with buffer loads (32 consecutive pixels per half-wave =
+//    128-byte lines, every activation read exactly once), are split into hi/lo in registers, and
+//    the next column's loads are issued as soon as a k-step's registers are consumed, so a whole
+//    tile of loads is always in flight behind the MFMAs.  No barriers after the weight load.
+//    Per 32-pixel tile: Cout/32 x K/16 x 3 MFMAs; A reads 4*Cout*K bytes of LDS (85 B/clk/CU at
+//    K = Cout = 192, under the 128 B/clk LDS rate), so the kernel is HBM-bound:
+//    bytes/pixel = 4*(Cin + Cout [+ Cout for the GDN/residual operand]).
+//
+// 2. conv3x3_narrow_kernel — 3x3 stride-1 convs with Cout <= 16 (g_s's last subpel conv, N -> 12).
+//    On MFMA a 12-row output wastes >80 % of a 64-row tile; as a direct convolution on the fp32
+//    VALU (exact fp32, packed 2-pixel FMAs) it needs 12*9 FMAs per input value, with a 16x32 output
+//    tile's input patch (+1 halo) staged through LDS in 8-channel chunks and weights read as
+//    wave-uniform scalars.
+//
+// 3. conv1x1_smallcin_kernel — 1x1 convs with Cin <= 4 (g_a's first point conv and skip, 3 -> N):
+//    write-bound; one pixel per lane, Cout outputs from scalar weights.
+#include "common.h"
+#include "kernels.h"
+
+namespace mlic {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+constexpr int PW_WAVES = 8;
+constexpr int PW_THREADS = PW_WAVES * 64;
+constexpr int LDS_BYTES = 160 * 1024;
+
+// buffer descriptor from a wave-uniform base (readfirstlane makes the uniformity provable: no
+// waterfall loops around the buffer ops)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  float* pb = reinterpret_cast<float*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, 0, bytes, 0x00020000);
+}
+
+// hides a scalar from loop-invariant hoisting / rematerialisation (96 live SGPR offsets would spill)
+__device__ __forceinline__ void opaque(uint32_t& v) { asm volatile("" : "+s"(v)); }
+
+template <int CIN>
+constexpr int pw_apitch() { return CIN + 8; }  // halves; +16 B per row spreads rows over the banks
+
+// MODE: 0 = bias only, 1 = GELU, 2 = GDN (x * rsqrt), 3 = IGDN (x * sqrt); residual add at run time
+template <int CIN, int CT, int MODE, bool RES>
+__global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, const _Float16* __restrict__ wh,
+                                                                  const _Float16* __restrict__ wl, int cin_pad) {
+  constexpr int KS = CIN / 16;
+  constexpr int APITCH = pw_apitch<CIN>();
+  constexpr int ROWS = CT * 32;
+  constexpr int A_SZ = ROWS * APITCH;
+  static_assert(CIN % 16 == 0 && 2 * A_SZ * 2 + ROWS * 4 <= LDS_BYTES, "pw_resident: weights must fit in LDS");
+  __shared__ __attribute__((aligned(16))) _Float16 sm[2 * A_SZ + 2 * ROWS];  // + fp32 bias[ROWS]
+  float* sbias = reinterpret_cast<float*>(sm + 2 * A_SZ);
+
+  const int tid = threadIdx.x;
+  constexpr int QPR = CIN / 8;  // 16-byte chunks per weight row
+  for (int id = tid; id < ROWS * QPR; id += PW_THREADS) {
+    const int row = id / QPR, q = id - row * QPR;
+    uint4 h = make_uint4(0, 0, 0, 0), l = make_uint4(0, 0, 0, 0);
+    if (row < P.Cout) {
+      h = *reinterpret_cast<const uint4*>(wh + (int64_t)row * cin_pad + 8 * q);
+      l = *reinterpret_cast<const uint4*>(wl + (int64_t)row * cin_pad + 8 * q);
+    }
+    *reinterpret_cast<uint4*>(sm + row * APITCH + 8 * q) = h;
+    *reinterpret_cast<uint4*>(sm + A_SZ + row * APITCH + 8 * q) = l;
+  }
+  for (int r = tid; r < ROWS; r += PW_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int HW = P.Ho * P.Wo;
+  const int tpi = (HW + 31) >> 5;  // 32-pixel tiles per image
+  const int ntiles = tpi * P.B;
+  const int tstride = gridDim.x * PW_WAVES;
+  int tile = blockIdx.x * PW_WAVES + wave;
+  if (tile >= ntiles) return;  // no barrier follows
+
+  constexpr bool square = MODE >= 2;  // GDN/IGDN convolve x*x
+  const float* xbase = P.seg[0].p;
+  const int64_t xbs = P.seg[0].bs;
+  const uint32_t hw4 = (uint32_t)HW * 4u;
+  const uint32_t img_bytes = (uint32_t)CIN * hw4;
+
+  // per-tile buffer descriptor over one image's CIN planes; per-lane pixel offset in voffset,
+  // the (uniform) channel offset in soffset
+  auto rsrc_of = [&](int t) { return make_rsrc(xbase + (int64_t)(t / tpi) * xbs, img_bytes); };
+  auto voff_of = [&](int t) {
+    const int b = t / tpi;
+    const int p = min(((t - b * tpi) << 5) + l32, HW - 1);
+    return (uint32_t)p * 4u + (uint32_t)(8 * h) * hw4;
+  };
+
+  // load ring: D = KS/2 k-steps ahead.  Slot j % D holds k-step j of the current tile until it is
+  // consumed, then receives k-step j + D (of this tile, or of the next one for j >= KS - D).
+  constexpr int D = KS / 2;
+  float ring[D][8];
+  {
+    const auto rs = rsrc_of(tile);
+    const uint32_t vo = voff_of(tile);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        ring[j][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (16 * j + i) * hw4, 0));
+  }
+
+  const _Float16* Ah = sm + l32 * APITCH + 8 * h;
+  const _Float16* Al = Ah + A_SZ;
+  for (; tile < ntiles; tile += tstride) {
+    int nt = tile + tstride;
+    if (nt >= ntiles) nt = tile;  // last tile: reload the current one (keeps every load unconditional)
+    const auto rsc = rsrc_of(tile);
+    const uint32_t voc = voff_of(tile);
+    const auto rsn = rsrc_of(nt);
+    const uint32_t von = voff_of(nt);
+
+    floatx16 acc[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
+    uint32_t so = (uint32_t)(16 * D) * hw4;  // channel byte offset of the next load, advanced load by load
+    opaque(so);
+
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      half8 bh, bl;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v = ring[j % D][i];
+        if (square) v *= v;
+        const _Float16 hv = (_Float16)v;
+        bh[i] = hv;
+        bl[i] = (_Float16)(v - (float)hv);
+      }
+      if (j == KS - D) {  // switch the stream to the next tile's k-step 0
+        so = 0;
+        opaque(so);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ring[j % D][i] = __builtin_bit_cast(float, j + D < KS ? __builtin_amdgcn_raw_buffer_load_b32(rsc, voc, so, 0)
+                                                              : __builtin_amdgcn_raw_buffer_load_b32(rsn, von, so, 0));
+        so += (i == 7) ? 9 * hw4 : hw4;
+        opaque(so);
+      }
+      // keep the reload here: the scheduler would otherwise hoist the ring's loads above the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      // co-tiles in pairs so consecutive MFMAs never chain on one accumulator
+#pragma unroll
+      for (int c = 0; c < CT; c += 2) {
+        const int c1 = (c + 1 < CT) ? c + 1 : c;
+        const half8 ah0 = *reinterpret_cast<const half8*>(Ah + c * 32 * APITCH + 16 * j);
+        const half8 al0 = *reinterpret_cast<const half8*>(Al + c * 32 * APITCH + 16 * j);
+        const half8 ah1 = *reinterpret_cast<const half8*>(Ah + c1 * 32 * APITCH + 16 * j);
+        const half8 al1 = *reinterpret_cast<const half8*>(Al + c1 * 32 * APITCH + 16 * j);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al0, bh, acc[c], 0, 0, 0);
+        if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al1, bh, acc[c1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bl, acc[c], 0, 0, 0);
+        if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bl, acc[c1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bh, acc[c], 0, 0, 0);
+        if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bh, acc[c1], 0, 0, 0);
+      }
+    }
+
+    // epilogue: buffer ops whose per-lane part is (pixel, lane half) and whose channel part is a
+    // uniform SGPR offset, so 96 stores need no 64-bit VGPR addresses
+    const int b = tile / tpi;
+    const int p = ((tile - b * tpi) << 5) + l32;
+    const uint32_t cs4 = (uint32_t)P.out_cs * 4u;
+    const uint32_t vo_out = (uint32_t)p * 4u + (uint32_t)(4 * h) * cs4;
+    const auto rs_out = make_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
+    constexpr bool gdn = MODE >= 2, igdn = MODE == 3, gelu = MODE == 1;
+    constexpr bool res = RES;
+    const auto rs_aux = make_rsrc(gdn ? P.aux + (int64_t)b * P.aux_bs : P.out, gdn ? (uint32_t)P.Cout * hw4 : 0u);
+    const uint32_t vo_aux = (uint32_t)p * 4u + (uint32_t)(4 * h) * hw4;
+    const auto rs_res = make_rsrc(res ? P.res + (int64_t)b * P.res_bs : P.out, res ? (uint32_t)P.Cout * cs4 : 0u);
+    const float* sb = sbias + 4 * h;  // per-lane base; the channel part folds into the ds_read offset
+    // per co-tile: issue the 16 aux / residual loads together, then one wait, then 16 stores
+    uint32_t so_o = 0, so_a = 0;  // channel byte offsets co_u * out_cs * 4 and co_u * HW * 4
+    if (p < HW) {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        float xa[16], xr[16];
+        uint32_t oo = so_o, oa = so_a;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (r > 0) {
+            const uint32_t step = ((r & 3) == 0) ? 5u : 1u;  // co_u = 32c + (r&3) + 8(r>>2)
+            oo += step * cs4;
+            oa += step * hw4;
+            opaque(oo);
+            opaque(oa);
+          }
+          if (gdn) xa[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_aux, vo_aux, oa, 0));
+          xr[r] = res ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, vo_out, oo, 0)) : 0.0f;
+        }
+        oo = so_o;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = c * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (r > 0) {
+            oo += (((r & 3) == 0) ? 5u : 1u) * cs4;
+            opaque(oo);
+          }
+          float v = acc[c][r];
+          v += sb[c * 32 + (r & 3) + 8 * (r >> 2)];
+          if (gelu) v = gelu_erf(v);
+          if (gdn) v = igdn ? xa[r] * sqrtf(v) : xa[r] * (1.0f / sqrtf(v));
+          v += xr[r];
+          if (c * 32 + 32 <= P.Cout || co < P.Cout)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
+        }
+        so_o += 32 * cs4;
+        so_a += 32 * hw4;
+        opaque(so_o);
+        opaque(so_a);
+      }
+    }
+  }
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return n;
+}
+
+bool pw_resident_ok(const ConvParams& P, int cin_pad) {
+  if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1) return false;
+  if (P.epi & ~(EPI_GELU | EPI_GDN | EPI_IGDN | EPI_SQUARE_IN | EPI_RES)) return false;
+  if ((P.epi & EPI_GELU) && (P.epi & (EPI_GDN | EPI_IGDN))) return false;
+  if (((P.epi & (EPI_GDN | EPI_IGDN)) != 0) != ((P.epi & EPI_SQUARE_IN) != 0)) return false;
+  if (P.Ho != P.H || P.Wo != P.W || P.seg[0].C != P.Cin || cin_pad != P.Cin) return false;
+  const int64_t HW = (int64_t)P.H * P.W;
+  if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
+  const int ct = (P.Cout + 31) / 32;
+  switch (P.Cin) {
+    case 96: return ct == 3;
+    case 128: return ct == 4;
+    case 160: return ct == 5;
+    case 192: return ct == 6;
+    default: return false;
+  }
+}
+
+template <int CIN, int CT>
+static void launch_pw(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
+  const int64_t ntiles = (int64_t)((P.Ho * P.Wo + 31) / 32) * P.B;
+  const int64_t want = (ntiles + PW_WAVES - 1) / PW_WAVES;
+  const dim3 grid((unsigned)std::min<int64_t>(want, (int64_t)num_cus()));
+  const int mode = (P.epi & EPI_GELU) ? 1 : (P.epi & EPI_GDN) ? 2 : (P.epi & EPI_IGDN) ? 3 : 0;
+  const bool res = (P.epi & EPI_RES) != 0;
+#define MLIC_PW(M, R) \
+  hipLaunchKernelGGL((pw_resident_kernel<CIN, CT, M, R>), grid, dim3(PW_THREADS), 0, st, P, wh, wl, cin_pad)
+  switch (mode * 2 + (res ? 1 : 0)) {
+    case 0: MLIC_PW(0, false); break;
+    case 1: MLIC_PW(0, true); break;
+    case 2: MLIC_PW(1, false); break;
+    case 3: MLIC_PW(1, true); break;
+    case 4: MLIC_PW(2, false); break;
+    case 5: MLIC_PW(2, true); break;
+    case 6: MLIC_PW(3, false); break;
+    default: MLIC_PW(3, true); break;
+  }
+#undef MLIC_PW
+  HIP_OK(hipGetLastError());
+}
+
+void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
+  MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
+  switch (P.Cin) {
+    case 96: launch_pw<96, 3>(P, wh, wl, cin_pad, st); break;
+    case 128: launch_pw<128, 4>(P, wh, wl, cin_pad, st); break;
+    case 160: launch_pw<160, 5>(P, wh, wl, cin_pad, st); break;
+    default: launch_pw<192, 6>(P, wh, wl, cin_pad, st); break;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 3x3 stride-1 pad-1 conv, Cout = COUT <= 16, exact fp32 on the VALU.
+constexpr int NR_TH = 16, NR_TW = 32, NR_CC = 8;
+constexpr int NR_PH = NR_TH + 2, NR_PW = NR_TW + 2;  // input patch (pitch NR_PW, even => 8-byte reads)
+constexpr int NR_PATCH = NR_CC * NR_PH * NR_PW;
+constexpr int NR_STAGE = (NR_PATCH + 255) / 256;
+
+template <int COUT>
+__global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
+  typedef float float2v __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) float sm[2 * NR_PATCH];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;  // 2 output pixels (2tx, 2tx+1) of row ty
+  const int ow0 = blockIdx.x * NR_TW, oh0 = blockIdx.y * NR_TH;
+  const int b = blockIdx.z;
+  const int H = P.H, W = P.W;
+  const int64_t HW = (int64_t)H * W;
+  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs;
+  const int nchunk = (P.Cin + NR_CC - 1) / NR_CC;
+
+  float stage[NR_STAGE];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int s = 0; s < NR_STAGE; ++s) {
+      const int e = tid + s * 256;
+      float v = 0.0f;
+      if (e < NR_PATCH) {
+        const int c = e / (NR_PH * NR_PW);
+        const int rem = e - c * (NR_PH * NR_PW);
+        const int py = rem / NR_PW, px = rem - py * NR_PW;
+        const int ci = ch * NR_CC + c;
+        const int ih = oh0 + py - 1, iw = ow0 + px - 1;
+        if (ci < P.Cin && ih >= 0 && ih < H && iw >= 0 && iw < W) v = x[(int64_t)ci * HW + (int64_t)ih * W + iw];
+      }
+      stage[s] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < NR_STAGE; ++s) {
+      const int e = tid + s * 256;
+      if (e < NR_PATCH) sm[buf * NR_PATCH + e] = stage[s];
+    }
+  };
+
+  float2v acc[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc[co] = float2v{0.0f, 0.0f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  const float* w = P.wpk;  // [9][Cin][COUT]
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int cur = ch & 1;
+    if (ch + 1 < nchunk) load(ch + 1);
+    const float* pb = sm + cur * NR_PATCH + ty * NR_PW + 2 * tx;
+    const int cmax = min(NR_CC, P.Cin - ch * NR_CC);
+    for (int c = 0; c < cmax; ++c) {
+      const int ci = ch * NR_CC + c;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const float2v x01 = *reinterpret_cast<const float2v*>(pb + c * NR_PH * NR_PW + dy * NR_PW);
+        const float2v x23 = *reinterpret_cast<const float2v*>(pb + c * NR_PH * NR_PW + dy * NR_PW + 2);
+        const float2v xs[3] = {x01, float2v{x01.y, x23.x}, x23};
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const float* wr = w + ((int64_t)(dy * 3 + dx) * P.Cin + ci) * COUT;
+#pragma unroll
+          for (int co = 0; co < COUT; ++co) acc[co] = __builtin_elementwise_fma(xs[dx], float2v{wr[co], wr[co]}, acc[co]);
+        }
+      }
+    }
+    if (ch + 1 < nchunk) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  const int oh = oh0 + ty;
+  if (oh >= P.Ho) return;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int ow = ow0 + 2 * tx + q;
+    if (ow >= P.Wo) continue;
+    const int p = oh * P.Wo + ow;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) conv_store(P, b, co, p, q ? acc[co].y : acc[co].x);
+  }
+}
+
+bool conv_narrow_ok(const ConvParams& P) {
+  return P.K == 3 && P.stride == 1 && P.pad == 1 && P.nseg == 1 && P.Cout == 12 && P.Ho == P.H && P.Wo == P.W &&
+         !(P.epi & EPI_SQUARE_IN);
+}
+
+void conv_narrow_forward(const ConvParams& P, hipStream_t st) {
+  MLIC_CHECK(conv_narrow_ok(P), "conv_narrow: unsupported shape");
+  dim3 grid((P.Wo + NR_TW - 1) / NR_TW, (P.Ho + NR_TH - 1) / NR_TH, P.B);
+  hipLaunchKernelGGL(conv3x3_narrow_kernel<12>, grid, dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// 1x1 conv (any stride, pad 0) with Cin <= 4: one output pixel per lane, exact fp32.
+template <int CIN>
+__global__ __launch_bounds__(256) void conv1x1_smallcin_kernel(ConvParams P) {
+  const int HWo = P.Ho * P.Wo;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (p >= HWo) return;
+  const int oh = p / P.Wo, ow = p - oh * P.Wo;
+  const int64_t HWi = (int64_t)P.H * P.W;
+  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs + (int64_t)(oh * P.stride) * P.W + ow * P.stride;
+  float xv[CIN];
+#pragma unroll
+  for (int c = 0; c < CIN; ++c) {
+    xv[c] = x[c * HWi];
+    if (P.epi & EPI_SQUARE_IN) xv[c] *= xv[c];
+  }
+  const float* w = P.wpk;  // [1][Cin][Cout]
+  for (int co = 0; co < P.Cout; ++co) {
+    float v = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) v = fmaf(xv[c], w[c * P.Cout + co], v);
+    conv_store(P, b, co, p, v);
+  }
+}
+
+bool conv_smallcin_ok(const ConvParams& P) {
+  return P.K == 1 && P.pad == 0 && P.nseg == 1 && P.Cin >= 1 && P.Cin <= 4;
+}
+
+void conv_smallcin_forward(const ConvParams& P, hipStream_t st) {
+  MLIC_CHECK(conv_smallcin_ok(P), "conv_smallcin: unsupported shape");
+  dim3 grid((P.Ho * P.Wo + 255) / 256, P.B);
+  switch (P.Cin) {
+    case 1: hipLaunchKernelGGL(conv1x1_smallcin_kernel<1>, grid, dim3(256), 0, st, P); break;
+    case 2: hipLaunchKernelGGL(conv1x1_smallcin_kernel<2>, grid, dim3(256), 0, st, P); break;
+    case 3: hipLaunchKernelGGL(conv1x1_smallcin_kernel<3>, grid, dim3(256), 0, st, P); break;
+    default: hipLaunchKernelGGL(conv1x1_smallcin_kernel<4>, grid, dim3(256), 0, st, P); break;
+  }
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace mlic

@@ -2,6 +2,8 @@
 #pragma once
 #include "common.h"
 
+#include <algorithm>
+
 namespace mlic {
 
 // implicit-GEMM conv on MFMA (conv_mfma.hip)
@@ -17,6 +19,42 @@ int conv_x3v2_variant(const ConvParams& P);
 void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad,
                    hipStream_t st);
+
+// specialised convs (conv_pw.hip)
+bool pw_resident_ok(const ConvParams& P, int cin_pad);
+void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
+bool conv_narrow_ok(const ConvParams& P);
+void conv_narrow_forward(const ConvParams& P, hipStream_t st);
+bool conv_smallcin_ok(const ConvParams& P);
+void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
+
+// kernel-family selection (conv_dispatch.cpp)
+enum ConvImpl : int { CONV_F32 = 0, CONV_X3 = 1, CONV_X3V2 = 2, CONV_PW = 3, CONV_NARROW = 4, CONV_SMALLCIN = 5 };
+struct ConvWeights {
+  const float* wpk;  // fp32 packed [K*K][Cin][Cout] (in ConvParams too)
+  const _Float16* wh;
+  const _Float16* wl;
+  int cin_pad;
+};
+int conv_select(const ConvParams& P, const ConvWeights& w, int precision);
+void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t st);
+
+// live-profiling categories (one per kernel family / tile instantiation)
+enum ProfCat : int {
+  PCAT_CONV_F32 = 0,     // 0..3  conv_mfma_kernel tiles (conv_variant)
+  PCAT_CONV_X3 = 4,      // 4..7  conv_f16x3_kernel tiles (conv_f16x3_variant)
+  PCAT_CONV_X3V2 = 8,    // 8..10 conv_x3v2_kernel tiles
+  PCAT_CONV_PW = 11,
+  PCAT_CONV_NARROW = 12,
+  PCAT_CONV_SMALLCIN = 13,
+  PCAT_DW = 14,
+  PCAT_LOCAL = 15,
+  PCAT_LINATT = 16,
+  PCAT_ELEM = 17,
+  PCAT_COUNT = 18
+};
+int conv_prof_cat(int impl, const ConvParams& P);
+const char* prof_cat_name(int cat);
 
 struct DwParams {
   Seg seg[MAXSEG];

@@ -299,15 +299,9 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
   const double outn = (double)L().B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * cin * w.K * w.K;
   const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  if (precision_ == PREC_F16X3_V2 && w.wh) {
-    timed(PROF_CONVX3 + conv_x3v2_variant(P), flops, bytes,
-          [&] { conv_x3v2_forward(P, w.wh, w.wl, w.cin_pad, L().st); }, w.name);
-  } else if (precision_ == PREC_F16X3 && w.wh) {
-    timed(PROF_CONVX3 + conv_f16x3_variant(P), flops, bytes,
-          [&] { conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, L().st); }, w.name);
-  } else {
-    timed(PROF_CONV + conv_variant(P), flops, bytes, [&] { conv_forward(P, L().st); }, w.name);
-  }
+  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad};
+  const int impl = conv_select(P, cw, precision_);
+  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st); }, w.name);
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {
@@ -333,7 +327,7 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
   P.gelu = gelu ? 1 : 0;
   P.B = L().B;
   const double outn = (double)L().B * c * P.Ho * P.Wo;
-  timed(PROF_DW, 18.0 * outn, 4.0 * ((double)L().B * c * P.H * P.W + outn), [&] { dw3x3(P, L().st); });
+  timed(PCAT_DW, 18.0 * outn, 4.0 * ((double)L().B * c * P.H * P.W + outn), [&] { dw3x3(P, L().st); });
 }
 
 // conv3x3 of the fork (modules/layers/conv.py:22-32): DepthWiseConv (dw 3x3 -> pw 1x1) by default,
@@ -494,7 +488,7 @@ View Model::local_context(const View& x, int i) {
   const size_t m = L().arena.mark();
   View n1 = alloc(C, H, W);
   const double pix = (double)L().B * H * W;
-  timed(PROF_ELEM, 8.0 * pix * C, 8.0 * pix * C, [&] {
+  timed(PCAT_ELEM, 8.0 * pix * C, 8.0 * pix * C, [&] {
     ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, L().B, L().st);
   });
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
@@ -514,12 +508,12 @@ View Model::local_context(const View& x, int i) {
     A.B = L().B;
     // per pixel: 2 heads x 25 query cells x 25 keys x hd (QK) + the same for AV
     const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
-    timed(PROF_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, L().st); });
+    timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, L().st); });
   }
   View f = conv1x1(t, p + ".fusion", 1, EPI_NONE);
   View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
   View n2 = alloc(2 * C, H, W);
-  timed(PROF_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
+  timed(PCAT_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
     ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, L().B, L().st);
   });
   View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
@@ -572,7 +566,7 @@ View Model::inter_context(const View& x, int i) {
   const int nsplit = ctx_splits(HW);
   float* part = L().arena.alloc((int64_t)L().B * heads * nsplit * hd * hd);
   float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
-  timed(PROF_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
+  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
     softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 0, L().st);
     softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 0, L().st);
     linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
@@ -599,7 +593,7 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   const size_t m = L().arena.mark();
   View x1n = alloc(D, H, W);
   View x1a = alloc(D, H, W);
-  timed(PROF_ELEM, 0.0, 16.0 * L().B * D * HW, [&] {
+  timed(PCAT_ELEM, 0.0, 16.0 * L().B * D * HW, [&] {
     ckbd_mask(x1.p, x1.bs, x1n.p, x1n.bs, D, H, W, L().B, 0, L().st);
     ckbd_mask(x1.p, x1.bs, x1a.p, x1a.bs, D, H, W, L().B, 1, L().st);
   });
@@ -612,7 +606,7 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   const int nsplit = ctx_splits(HW);
   float* part = L().arena.alloc((int64_t)L().B * heads * nsplit * hd * hd);
   float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
-  timed(PROF_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
+  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
     softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 1, L().st);
     softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 2, L().st);
     linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
@@ -765,7 +759,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.sym = d_sym + (int64_t)phase_id * L().B * n_per;
           Q.idx = d_idx + (int64_t)phase_id * L().B * n_per;
         }
-        timed(PROF_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); });
+        timed(PCAT_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); });
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
       lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
@@ -791,7 +785,7 @@ void Model::eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym) {
   P.H = z.H;
   P.W = z.W;
   P.B = L().B;
-  timed(PROF_ELEM, 0.0, 12.0 * L().B * z.C * z.H * z.W, [&] { eb_forward(P, L().st); });
+  timed(PCAT_ELEM, 0.0, 12.0 * L().B * z.C * z.H * z.W, [&] { eb_forward(P, L().st); });
 }
 
 template <class F>

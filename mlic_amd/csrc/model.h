@@ -56,11 +56,8 @@ class Arena {
   bool dry_ = false;
 };
 
-// live per-kernel-family timing with HIP events on the executor's stream (bench.py roofline)
-// categories 0..3 = conv_mfma_kernel (fp32) tile instantiations, 4..7 = conv_f16x3_kernel ones
-enum ProfCat : int {
-  PROF_CONV = 0, PROF_CONVX3 = 4, PROF_DW = 8, PROF_LOCAL = 9, PROF_LINATT = 10, PROF_ELEM = 11, PROF_NCAT = 12
-};
+// live per-kernel-family timing with HIP events on the executor's stream (bench.py roofline);
+// categories: ProfCat in kernels.h
 struct ProfStat {
   int64_t launches = 0;
   double ms = 0, flops = 0, bytes = 0;
@@ -150,7 +147,7 @@ class Model {
   std::vector<EncodedImage> enc_all_;
   std::vector<std::unique_ptr<Lane>> lanes_;
   int nlanes_ = 2;
-  int precision_ = PREC_F16X3;
+  int precision_ = PREC_F16X3_V2;
   bool prof_ = false;
   static thread_local Lane* tl_lane_;
   Lane& L() const { return *tl_lane_; }

@@ -1,0 +1,9 @@
+cd "$GRAFT_REPO_ROOT"
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 300 python -m pytest tests/test_gpu_conv.py -q -m gpu -x > gpurun_out/conv_tests_10.log 2>&1
+rc=$?; echo "conv tests rc=$rc" >> gpurun_out/conv_tests_10.log; if fatal $rc; then exit $rc; fi
+timeout -k 10 300 python tools/conv_bench.py 2 3 > gpurun_out/conv_bench_10.log 2>&1 || exit $?
+timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -q -m gpu > gpurun_out/gpu_tests_10.log 2>&1
+rc=$?; echo "tests rc=$rc" >> gpurun_out/gpu_tests_10.log; if fatal $rc; then exit $rc; fi
+timeout -k 10 600 python bench.py --no-cpu-baseline --steps 2 --layers-out gpurun_out/layers_10.tsv > gpurun_out/bench_10.json 2> gpurun_out/bench_10.err || exit $?
+echo done

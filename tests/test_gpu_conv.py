@@ -1,0 +1,106 @@
+"""Each conv kernel family against a plain PyTorch fp32 reference (F.conv2d + the epilogue), through
+the C-ABI entry mlic_conv_run.  Shapes: the layer types of MLIC++ that each family serves
+(g_a/g_s point convs and GDN/IGDN, subpel 3x3 convs with PixelShuffle, the N -> 12 output conv,
+the 3 -> N input convs, latent-resolution context GEMMs), plus ragged pixel counts."""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+GELU, GDN, IGDN, RES, SHUFFLE, SQUARE = 1, 2, 4, 64, 128, 256
+F32, X3, X3V2, PW, NARROW, SMALLCIN, AUTO = 0, 1, 2, 3, 4, 5, -1
+
+
+def reference(x, w, b, stride, epi, res):
+    y = F.conv2d((x * x) if epi & SQUARE else x, w, b, stride=stride, padding=w.shape[-1] // 2)
+    if epi & GELU:
+        y = F.gelu(y)
+    if epi & GDN:
+        y = x * torch.rsqrt(y)
+    if epi & IGDN:
+        y = x * torch.sqrt(y)
+    if epi & SHUFFLE:
+        y = F.pixel_shuffle(y, 2)
+    if epi & RES:
+        y = y + res
+    return y
+
+
+def run(impl, B, Cin, Cout, H, W, K, stride=1, epi=0, seed=0):
+    from mlic_amd import _lib
+    g = torch.Generator().manual_seed(seed)
+    dev = torch.device("cuda")
+    x = (torch.rand(B, Cin, H, W, generator=g) - 0.5).to(dev)
+    w = ((torch.rand(Cout, Cin, K, K, generator=g) - 0.5) / (Cin * K * K) ** 0.5).to(dev)
+    b = (torch.rand(Cout, generator=g) - 0.5).to(dev)
+    if epi & (GDN | IGDN):  # GDN: gamma >= 0, beta > 0 (compressai reparametrisation keeps them so)
+        x = x * 4
+        w = w.abs() * 0.1
+        b = 1.0 + b.abs()
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    oshape = (B, Cout // 4, 2 * Ho, 2 * Wo) if epi & SHUFFLE else (B, Cout, Ho, Wo)
+    res = (torch.rand(*oshape, generator=g) - 0.5).to(dev) if epi & RES else None
+    y = torch.full(oshape, float("nan"), device=dev)
+    aux = x if epi & (GDN | IGDN) else None
+    st = torch.cuda.current_stream().cuda_stream
+    ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    _lib.call("mlic_conv_run", C.c_void_p(st), impl, ptr(x), ptr(w), ptr(b), ptr(y), B, Cin, Cout, H, W, K, stride,
+              epi, ptr(aux), ptr(res))
+    ref = reference(x.double(), w.double(), b.double(), stride, epi, res.double() if res is not None else None)
+    return y, ref.float()
+
+
+def check(y, ref, rtol=2e-5):
+    assert torch.isfinite(y).all(), "unwritten or non-finite outputs"
+    err = (y - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= rtol * scale + 1e-6, f"max err {err:.3e} (scale {scale:.3e})"
+
+
+@pytest.mark.parametrize("cin", [96, 128, 160, 192])
+def test_pw_resident_sizes(cin):
+    check(*run(PW, 2, cin, cin, 48, 80, 1))
+
+
+@pytest.mark.parametrize("epi", [0, GELU, GDN | SQUARE, IGDN | SQUARE, GELU | RES, GDN | SQUARE | RES])
+def test_pw_resident_epilogues(epi):
+    check(*run(PW, 2, 192, 192, 36, 60, 1, epi=epi))
+
+
+def test_pw_resident_ragged_and_many_tiles():
+    check(*run(PW, 3, 192, 192, 37, 53, 1))   # 1961 px: tail tile per image
+    check(*run(PW, 2, 192, 192, 136, 240, 1))  # > 2048 tiles: every wave loops
+
+
+@pytest.mark.parametrize("epi", [0, SHUFFLE])
+def test_narrow(epi):
+    check(*run(NARROW, 2, 192, 12, 40, 72, 3, epi=epi))
+    check(*run(NARROW, 1, 96, 12, 19, 45, 3, epi=epi))
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_smallcin(stride):
+    check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride))
+
+
+@pytest.mark.parametrize("impl", [F32, X3, X3V2])
+@pytest.mark.parametrize("shape", [
+    (2, 192, 768, 24, 40, 3, 1, SHUFFLE | GELU),  # subpel conv
+    (2, 192, 192, 33, 47, 1, 1, GDN | SQUARE),     # GDN on the generic tiles
+    (2, 960, 320, 17, 30, 1, 1, 0),                # entropy-parameters GEMM
+    (2, 288, 96, 17, 30, 5, 1, 0),                 # inter-context 5x5 reprojection
+    (1, 192, 192, 34, 60, 3, 2, GELU),             # strided 3x3
+])
+def test_generic_tiles(impl, shape):
+    B, cin, cout, H, W, K, s, epi = shape
+    check(*run(impl, B, cin, cout, H, W, K, stride=s, epi=epi))
+
+
+def test_auto_matches_selected_family():
+    y, ref = run(AUTO, 2, 192, 192, 136, 240, 1, epi=GELU)
+    check(y, ref)
+    y2, _ = run(PW, 2, 192, 192, 136, 240, 1, epi=GELU)
+    assert torch.equal(y, y2)

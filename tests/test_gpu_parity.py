@@ -5,6 +5,7 @@ path; checkerboard / mask / slice bookkeeping bit-exact; tensors to fp32 summati
 """
 import hashlib
 import math
+import os
 
 import numpy as np
 import pytest
@@ -208,6 +209,39 @@ def test_1080p_parity_and_roundtrip():
     # the coder never costs more than the likelihood estimate (+ a small overhead); it can cost less
     # where escape (bypass) coding of outliers is cheaper than -log2 of the 1e-9 likelihood floor
     assert 8 * nbytes / (H * W) <= bg * 1.01 + 0.01
+
+
+def test_kodak_size_parity():
+    """BASELINE config 1 shape (768x512) and its portrait twin, vs the CPU oracle."""
+    name = "MLICPP_L"
+    sd = synthetic.synth_state_dict(name, 0)
+    m = ref.RefMLIC(name, sd)
+    for H, W in ((512, 768), (768, 512)):
+        x = synthetic.synth_image(H, W, 7)
+        o = m.forward(x)
+        out = net_for(name)(x.to(DEV))
+        torch.cuda.synchronize()
+        bc = ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"], o["likelihoods"]["z_likelihoods"], H * W)
+        assert abs(bpp(out, H * W) - bc) <= 1e-3
+        assert abs(ref.psnr_uint8(x, out["x_hat"].cpu()) - ref.psnr_uint8(x, o["x_hat"])) <= 0.01
+
+
+def test_file_format_roundtrip(tmp_path):
+    """utils/testing.py:203-230 semantics: pad, compress, file, decompress, crop (non-64 size)."""
+    from mlic_amd import bitstream
+    net = net_for("MLICPP_S")
+    net.update()
+    img = synthetic.synth_image(120, 200, 3).to(DEV)  # padded to 128 x 256 inside
+    r = bitstream.code_image(net, img)
+    assert r["x_hat"].shape == img.shape
+    fwd = net(bitstream.pad64(img))["x_hat"][:, :, :120, :200]
+    assert torch.equal(r["x_hat"], fwd)
+    out = net.compress(bitstream.pad64(img))
+    path = str(tmp_path / "img.bin")
+    n = bitstream.write_file(path, 120, 200, out)
+    assert os.path.getsize(path) == n == r["bytes"]
+    hdr, strings, shape = bitstream.read_file(path)
+    assert tuple(hdr) == (120, 200) and strings == [[out["strings"][0][0]], [out["strings"][1][0]]]
 
 
 def test_cpu_tensor_raises():

@@ -19,7 +19,9 @@ SHAPES = [
 ]
 
 
-EXTRA = [("g_s.7 subpel 3x3 192->12 @544x960", 8, 192, 12, 544, 960, 3, 1, 1)]
+EXTRA = [("g_s.7 subpel 3x3 192->12 @544x960", 8, 192, 12, 544, 960, 3, 1, 1),
+         ("g_a.0 skip 1x1/2 3->192 @1088x1920", 8, 3, 192, 1088, 1920, 1, 2, 0),
+         ("g_a.0 pw 3->192 @544x960", 8, 3, 192, 544, 960, 1, 1, 0)]
 
 
 def main():
@@ -29,7 +31,9 @@ def main():
         for impl in impls:
             ms, tf = C.c_double(), C.c_double()
             _lib.call("mlic_bench_conv", impl, B, Cin, Cout, H, W, K, s, sh, 10, C.byref(ms), C.byref(tf))
-            row.append(f"impl{impl}: {ms.value:8.3f} ms {tf.value:7.1f} TF/s")
+            Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+            gbs = 4.0 * B * (Cin * H * W + Cout * Ho * Wo) / (ms.value * 1e-3) / 1e9
+            row.append(f"impl{impl}: {ms.value:8.3f} ms {tf.value:7.1f} TF/s {gbs:6.0f} GB/s")
         print("  ".join(row), flush=True)
 
 

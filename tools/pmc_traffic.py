@@ -1,0 +1,45 @@
+"""HBM traffic per launch of one kernel from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE are
+collected in separate passes, MI355X_MICROARCH.md §rocprofv3 PMC slots).
+
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <out.json> [key=value ...]
+
+FETCH_SIZE / WRITE_SIZE are in KiB (TCC_EA0 requests).  gfx950 caveat (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE reads exactly half the bytes of a 16-byte-per-lane streaming read; other access widths
+are uncalibrated, so we report the raw sum and, separately, the sum with FETCH doubled (upper bound).
+Infinity-Cache hits are counted too (they are memory-side requests).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_launch(d, counter, kernel):
+    vals = []
+    for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(fn)):
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+                vals.append(float(r["Counter_Value"]) * 1024.0)
+    return sum(vals) / len(vals) if vals else None, len(vals)
+
+
+def main():
+    fetch_dir, write_dir, kernel, out = sys.argv[1:5]
+    extra = dict(kv.split("=", 1) for kv in sys.argv[5:])
+    for k in ("H", "W", "batch"):
+        if k in extra:
+            extra[k] = int(extra[k])
+    f, nf = per_launch(fetch_dir, "FETCH_SIZE", kernel)
+    w, nw = per_launch(write_dir, "WRITE_SIZE", kernel)
+    res = dict(extra, kernel=kernel, launches_fetch=nf, launches_write=nw,
+               fetch_bytes_per_launch=f, write_bytes_per_launch=w,
+               conv_hbm_bytes_per_launch=(f + w) if f is not None and w is not None else None,
+               conv_hbm_bytes_per_launch_fetch_doubled=(2 * f + w) if f is not None and w is not None else None)
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
