@@ -89,6 +89,9 @@ int mlic_profile_category_name(int cat, char* buf, size_t cap);
  * Synchronous on `stream`. */
 int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,
                   int Cout, int H, int W, int K, int stride, int epi, const float* aux, const float* res);
+/* depthwise 3x3 (pad 1, stride 1|2, optional GELU); w [C][9]; synchronous on `stream` */
+int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W,
+                int stride, int gelu);
 /* impl 0..2 as mlic_conv_run, 3 = the model's choice */
 int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
                     double* ms_per, double* tflops);

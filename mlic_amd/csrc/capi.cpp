@@ -149,7 +149,7 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
 
 int mlic_set_precision(mlic_model* m, int precision) {
   return guard([&] {
-    MLIC_CHECK(precision >= PREC_F32 && precision <= PREC_F16X3_V2, "precision must be 0 (f32), 1 or 2 (f16x3)");
+    MLIC_CHECK(precision >= 0 && precision <= 3, "precision must be 0 (f32), 1, 2 or 3 (f16x3 tiles v1/v2/v3)");
     m->impl->set_precision(precision);
   });
 }
@@ -223,7 +223,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     P.out_cs = (int64_t)Ho * Wo;
     P.epi = shuffle ? EPI_SHUFFLE : 0;
     const ConvWeights cw{wp, wh, wl, cin_pad};
-    const int which = impl == 3 ? conv_select(P, cw, 2) : impl;  // 3 = what the model runs (precision 2)
+    const int which = impl == 3 ? conv_select(P, cw, 2) : impl == 7 ? conv_select(P, cw, 3) : impl;  // 3/7 = model choice at precision 2/3
     auto launch = [&] { conv_run(which, P, cw, nullptr); };
     launch();
     HIP_OK(hipDeviceSynchronize());
@@ -295,6 +295,21 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     HIP_OK(hipFreeAsync(wh, st));
     HIP_OK(hipFreeAsync(wl, st));
     HIP_OK(hipStreamSynchronize(st));
+  });
+}
+
+int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W,
+                int stride, int gelu) {
+  return guard([&] {
+    DwParams P{};
+    P.nseg = 1;
+    P.seg[0] = {x, C, (int64_t)C * H * W};
+    P.C = C; P.H = H; P.W = W; P.stride = stride;
+    P.Ho = (H - 1) / stride + 1;
+    P.Wo = (W - 1) / stride + 1;
+    P.w = w; P.bias = bias; P.out = y; P.out_bs = (int64_t)C * P.Ho * P.Wo; P.gelu = gelu; P.B = B;
+    dw3x3(P, (hipStream_t)stream);
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
   });
 }
 

@@ -85,12 +85,86 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
   }
 }
 
+// stride-1 fast path: 32x128 output tile, the (34 x 136)-float input patch staged with aligned
+// float4 loads (patch column 0 = input column ox0 - 4, so each float4 is wholly inside or outside
+// the image when W % 4 == 0), and each thread computes a 4x4 output block from a sliding 3-row
+// register window: 6 patch rows x (1 float4 + 2 scalars) LDS reads for 16 outputs.
+constexpr int DWF_TH = 32, DWF_TW = 128, DWF_PR = DWF_TH + 2, DWF_PQ = DWF_TW / 4 + 2;  // patch rows, float4s/row
+__global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
+  __shared__ float4 tile[DWF_PR * DWF_PQ];
+  const int c = blockIdx.y, b = blockIdx.z;
+  const int ntx = (P.Wo + DWF_TW - 1) / DWF_TW;
+  const int ox0 = (blockIdx.x % ntx) * DWF_TW, oy0 = (blockIdx.x / ntx) * DWF_TH;
+  int sg = 0, c0 = 0;
+  while (sg + 1 < P.nseg && c >= c0 + P.seg[sg].C) { c0 += P.seg[sg].C; ++sg; }
+  const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
+  const int W4 = P.W >> 2;
+  const float4* src4 = reinterpret_cast<const float4*>(src);
+  for (int i = threadIdx.x; i < DWF_PR * DWF_PQ; i += 256) {
+    const int r = i / DWF_PQ, q = i - r * DWF_PQ;
+    const int gy = oy0 - 1 + r, gq = (ox0 >> 2) - 1 + q;  // float4 column
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gy >= 0 && gy < P.H && gq >= 0 && gq < W4) v = src4[(int64_t)gy * W4 + gq];
+    tile[i] = v;
+  }
+  __syncthreads();
+  float w[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w[k] = P.w[c * 9 + k];
+  const float bias = P.bias ? P.bias[c] : 0.0f;
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;  // 4 columns x 4 rows per thread
+  const float* tf = reinterpret_cast<const float*>(tile);
+  constexpr int PITCH = DWF_PQ * 4;
+  // window rows: input cols 4cg-1 .. 4cg+4  <->  patch cols 4cg+3 .. 4cg+8
+  float win[3][6];
+  auto load_row = [&](int pr, float* dst) {
+    const float* rp = tf + pr * PITCH + 4 * cg + 3;
+    const float4 m = tile[pr * DWF_PQ + cg + 1];
+    dst[0] = rp[0];
+    dst[1] = m.x; dst[2] = m.y; dst[3] = m.z; dst[4] = m.w;
+    dst[5] = rp[5];
+  };
+  load_row(4 * rg, win[0]);
+  load_row(4 * rg + 1, win[1]);
+  float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)c * P.Ho * P.Wo;
+  const int ox = ox0 + 4 * cg;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    load_row(4 * rg + r + 2, win[(r + 2) % 3]);
+    float o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], win[(r + ky) % 3][q + kx], acc);
+      float v = acc + bias;
+      if (P.gelu) v = gelu_erf(v);
+      o[q] = v;
+    }
+    const int oy = oy0 + 4 * rg + r;
+    if (oy < P.Ho && ox < P.Wo)  // Wo % 4 == 0: a strip is wholly inside or outside
+      *reinterpret_cast<float4*>(dst + (int64_t)oy * P.Wo + ox) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 void dw3x3(const DwParams& P, hipStream_t st) {
   MLIC_CHECK(P.stride == 1 || P.stride == 2, "dw stride");
   MLIC_CHECK(P.Ho == (P.H - 1) / P.stride + 1 && P.Wo == (P.W - 1) / P.stride + 1, "dw output size");
   int tot = 0;
-  for (int i = 0; i < P.nseg; ++i) tot += P.seg[i].C;
+  bool aligned = (P.W % 4) == 0 && (reinterpret_cast<uintptr_t>(P.out) % 16) == 0 && (P.out_bs % 4) == 0;
+  for (int i = 0; i < P.nseg; ++i) {
+    tot += P.seg[i].C;
+    aligned = aligned && (reinterpret_cast<uintptr_t>(P.seg[i].p) % 16) == 0 && (P.seg[i].bs % 4) == 0;
+  }
   MLIC_CHECK(tot == P.C, "dw segments");
+  if (P.stride == 1 && aligned) {
+    const int ntx = (P.Wo + DWF_TW - 1) / DWF_TW, nty = (P.Ho + DWF_TH - 1) / DWF_TH;
+    hipLaunchKernelGGL(dw3x3_s1_vec_kernel, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
+    HIP_OK(hipGetLastError());
+    return;
+  }
   const int TH = P.stride == 1 ? DW_TH1 : DW_TH2;
   const int ntx = (P.Wo + DW_TW - 1) / DW_TW, nty = (P.Ho + TH - 1) / TH;
   if (P.stride == 1) hipLaunchKernelGGL(dw3x3_kernel<1>, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);

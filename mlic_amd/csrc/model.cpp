@@ -99,6 +99,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
       w.w = dst;
       w.C = shape(i, 0);
       MLIC_CHECK(shape(i, 2) == 3 && shape(i, 3) == 3, "depthwise kernels are 3x3");
+      w.name = base;
       dws_[base] = w;
     } else if (ends_with(k, ".weight") && (ndims[i] == 4 || ndims[i] == 2) &&
                k.find("entropy_bottleneck") == std::string::npos && k.find("norm") == std::string::npos) {
@@ -327,7 +328,7 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
   P.gelu = gelu ? 1 : 0;
   P.B = L().B;
   const double outn = (double)L().B * c * P.Ho * P.Wo;
-  timed(PCAT_DW, 18.0 * outn, 4.0 * ((double)L().B * c * P.H * P.W + outn), [&] { dw3x3(P, L().st); });
+  timed(PCAT_DW, 18.0 * outn, 4.0 * ((double)L().B * c * P.H * P.W + outn), [&] { dw3x3(P, L().st); }, w.name);
 }
 
 // conv3x3 of the fork (modules/layers/conv.py:22-32): DepthWiseConv (dw 3x3 -> pw 1x1) by default,
@@ -875,12 +876,14 @@ std::string Model::profile_layers() {
     }
   std::vector<std::pair<std::string, Acc>> v(acc.begin(), acc.end());
   std::sort(v.begin(), v.end(), [](auto& x, auto& y) { return x.second.ms > y.second.ms; });
-  std::string out = "layer\tcat\tlaunches\tms\tGFLOP\tTFLOP/s\n";
+  std::string out = "layer\tkernel\tlaunches\tms\tGFLOP\tTFLOP/s\tGB\tGB/s\n";
   char buf[512];
   for (auto& kv : v) {
     const Acc& a = kv.second;
-    std::snprintf(buf, sizeof buf, "%s\t%d\t%lld\t%.4f\t%.3f\t%.2f\n", kv.first.c_str(), a.cat, (long long)a.n, a.ms,
-                  a.flops / 1e9, a.ms > 0 ? a.flops / (a.ms * 1e-3) / 1e12 : 0.0);
+    std::snprintf(buf, sizeof buf, "%s\t%s\t%lld\t%.4f\t%.3f\t%.2f\t%.3f\t%.0f\n", kv.first.c_str(),
+                  prof_cat_name(a.cat), (long long)a.n, a.ms, a.flops / 1e9,
+                  a.ms > 0 ? a.flops / (a.ms * 1e-3) / 1e12 : 0.0, a.bytes / 1e9,
+                  a.ms > 0 ? a.bytes / (a.ms * 1e-3) / 1e9 : 0.0);
     out += buf;
   }
   return out;

@@ -36,6 +36,7 @@ struct DwW {
   const float* w = nullptr;  // [C][9]
   const float* b = nullptr;
   int C = 0;
+  std::string name;
 };
 
 // arena: stream-ordered bump allocator; a dry run sizes it

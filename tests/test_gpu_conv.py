@@ -11,7 +11,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 GELU, GDN, IGDN, RES, SHUFFLE, SQUARE = 1, 2, 4, 64, 128, 256
-F32, X3, X3V2, PW, NARROW, SMALLCIN, AUTO = 0, 1, 2, 3, 4, 5, -1
+F32, X3, X3V2, PW, NARROW, SMALLCIN, X3V3, AUTO = 0, 1, 2, 3, 4, 5, 6, -1
 
 
 def reference(x, w, b, stride, epi, res):
@@ -86,13 +86,15 @@ def test_smallcin(stride):
     check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride))
 
 
-@pytest.mark.parametrize("impl", [F32, X3, X3V2])
+@pytest.mark.parametrize("impl", [F32, X3, X3V2, X3V3])
 @pytest.mark.parametrize("shape", [
     (2, 192, 768, 24, 40, 3, 1, SHUFFLE | GELU),  # subpel conv
     (2, 192, 192, 33, 47, 1, 1, GDN | SQUARE),     # GDN on the generic tiles
     (2, 960, 320, 17, 30, 1, 1, 0),                # entropy-parameters GEMM
     (2, 288, 96, 17, 30, 5, 1, 0),                 # inter-context 5x5 reprojection
     (1, 192, 192, 34, 60, 3, 2, GELU),             # strided 3x3
+    (1, 96, 64, 9, 13, 3, 1, 0),                   # K-steps 27: odd count, tiny grid
+    (1, 32, 48, 8, 8, 1, 1, 0),                    # a single K-step
 ])
 def test_generic_tiles(impl, shape):
     B, cin, cout, H, W, K, s, epi = shape
@@ -104,3 +106,29 @@ def test_auto_matches_selected_family():
     check(y, ref)
     y2, _ = run(PW, 2, 192, 192, 136, 240, 1, epi=GELU)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 192, 64, 256, 1, 0),   # vectorised stride-1 path, 2 x 2 tiles
+    (2, 192, 40, 100, 1, 1),   # W % 4 == 0, ragged tiles, GELU
+    (1, 96, 37, 53, 1, 0),     # W % 4 != 0: generic path
+    (2, 192, 64, 96, 2, 0),    # stride 2
+    (1, 3, 65, 97, 2, 0),      # 3-channel stride-2 input conv, odd sizes
+])
+def test_depthwise(shape):
+    from mlic_amd import _lib
+    B, Cn, H, W, s, gelu = shape
+    g = torch.Generator().manual_seed(1)
+    dev = torch.device("cuda")
+    x = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
+    w = (torch.rand(Cn, 1, 3, 3, generator=g) - 0.5).to(dev)
+    b = (torch.rand(Cn, generator=g) - 0.5).to(dev)
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    y = torch.full((B, Cn, Ho, Wo), float("nan"), device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("mlic_dw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()),
+              C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()), B, Cn, H, W, s, gelu)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=s, padding=1, groups=Cn)
+    if gelu:
+        ref = F.gelu(ref)
+    check(y, ref.float(), rtol=1e-6)
