@@ -141,6 +141,8 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    hs = [C.c_double() for _ in range(3)]
+    _lib.call("mlic_host_stats", net._handle, *[C.byref(v) for v in hs], 1)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         c, d = step()
@@ -149,6 +151,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    _lib.call("mlic_host_stats", net._handle, *[C.byref(v) for v in hs], 1)
+    host = {k: round(v.value / a.steps, 2) for k, v in zip(("rans_encode", "rans_decode", "gpu_wait"), hs)}
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -246,6 +250,8 @@ def main():
                          "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3)},
             "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
+            "host_thread_ms_per_step": host,
+            "lanes": a.lanes,
             "quality": {"bpp_file_mean": round(float(rec[:, 1].mean()), 5),
                         "psnr_u8_mean": round(float(rec[:, 2].mean()), 4), "images": int(rec.shape[0])},
         }

@@ -80,6 +80,8 @@ int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, dou
 int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written);
 
 int mlic_profile_categories(int* n);
+/* host time summed over threads since the last reset: rANS encode, rANS decode, waits on the GPU */
+int mlic_host_stats(mlic_model* m, double* enc_ms, double* dec_ms, double* wait_ms, int reset);
 int mlic_profile_category_name(int cat, char* buf, size_t cap);
 
 /* kernel-level entry points (bit-exact tests, micro-benchmarks) */

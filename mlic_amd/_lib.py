@@ -45,6 +45,7 @@ def _sig(lib):
         "mlic_bench_conv": [i, i, i, i, i, i, i, i, i, i, P(C.c_double), P(C.c_double)],
         "mlic_profile_read": [p, i, P(i64), P(C.c_double), P(C.c_double), P(C.c_double)],
         "mlic_profile_categories": [P(i)],
+        "mlic_host_stats": [p, P(C.c_double), P(C.c_double), P(C.c_double), i],
         "mlic_profile_category_name": [i, p, sz],
         "mlic_conv_run": [p, i, p, p, p, p, i, i, i, i, i, i, i, i, p, p],
         "mlic_dw_run": [p, p, p, p, p, i, i, i, i, i, i],

@@ -244,6 +244,20 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
   });
 }
 
+int mlic_host_stats(mlic_model* m, double* enc_ms, double* dec_ms, double* wait_ms, int reset) {
+  return guard([&] {
+    HostStats& h = m->impl->host_stats();
+    *enc_ms = h.enc_ns.load() * 1e-6;
+    *dec_ms = h.dec_ns.load() * 1e-6;
+    *wait_ms = h.wait_ns.load() * 1e-6;
+    if (reset) {
+      h.enc_ns = 0;
+      h.dec_ns = 0;
+      h.wait_ns = 0;
+    }
+  });
+}
+
 int mlic_profile_categories(int* n) {
   return guard([&] { *n = PCAT_COUNT; });
 }

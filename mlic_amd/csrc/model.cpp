@@ -491,7 +491,7 @@ View Model::local_context(const View& x, int i) {
   const double pix = (double)L().B * H * W;
   timed(PCAT_ELEM, 8.0 * pix * C, 8.0 * pix * C, [&] {
     ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, L().B, L().st);
-  });
+  }, p + ".norm1");
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
   View t = alloc(25 * C, H, W);
   {
@@ -509,14 +509,14 @@ View Model::local_context(const View& x, int i) {
     A.B = L().B;
     // per pixel: 2 heads x 25 query cells x 25 keys x hd (QK) + the same for AV
     const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
-    timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, L().st); });
+    timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, L().st); }, p + ".attn");
   }
   View f = conv1x1(t, p + ".fusion", 1, EPI_NONE);
   View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
   View n2 = alloc(2 * C, H, W);
   timed(PCAT_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
     ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, L().B, L().st);
-  });
+  }, p + ".norm2");
   View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
   conv({h1}, cw(p + ".mlp.fc2"), 1, 0, out, EPI_NONE, nullptr, &pj);
   L().arena.release(m);
@@ -571,7 +571,7 @@ View Model::inter_context(const View& x, int i) {
     softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 0, L().st);
     softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 0, L().st);
     linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
-  });
+  }, p + ".attn");
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
   conv({att}, rp, 1, 2, a, EPI_NONE);
@@ -597,7 +597,7 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   timed(PCAT_ELEM, 0.0, 16.0 * L().B * D * HW, [&] {
     ckbd_mask(x1.p, x1.bs, x1n.p, x1n.bs, D, H, W, L().B, 0, L().st);
     ckbd_mask(x1.p, x1.bs, x1a.p, x1a.bs, D, H, W, L().B, 1, L().st);
-  });
+  }, p + ".ckbd");
   View q = qkv_branch(x1n, p + ".queries");
   View k = qkv_branch(x1a, p + ".keys");
   View v = qkv_branch(x2, p + ".values");
@@ -611,7 +611,7 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
     softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 1, L().st);
     softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 2, L().st);
     linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
-  });
+  }, p + ".attn");
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
   conv({att}, rp, 1, 2, a, EPI_NONE);
@@ -663,16 +663,23 @@ void Model::lrp(const std::vector<View>& ins, const std::string& kind, int i, co
 // ------------------------------------------------------------------------------------- phases
 class PhaseDecoder {
  public:
-  PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym, int32_t* h_idx)
-      : t_(t), h_sym_(h_sym), h_idx_(h_idx) {
+  PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym, int32_t* h_idx,
+               HostStats* hs)
+      : t_(t), h_sym_(h_sym), h_idx_(h_idx), hs_(hs) {
     dec_.resize(B);
     for (int b = 0; b < B; ++b) dec_[b].set_stream(y[b], ylen[b]);
   }
   void run(int64_t n_per, hipStream_t st, int32_t* d_idx, int32_t* d_sym) {
     const int B = (int)dec_.size();
     HIP_OK(hipMemcpyAsync(h_idx_, d_idx, sizeof(int32_t) * n_per * B, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    auto work = [&](int b) { dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per); };
+    {
+      HostStats::Scope w{hs_->wait_ns};
+      HIP_OK(hipStreamSynchronize(st));
+    }
+    auto work = [&](int b) {
+      HostStats::Scope d{hs_->dec_ns};
+      dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per);
+    };
     if (B == 1) {
       work(0);
     } else {
@@ -688,6 +695,7 @@ class PhaseDecoder {
   const CdfTables* t_;
   int32_t* h_sym_;
   int32_t* h_idx_;
+  HostStats* hs_;
 };
 
 // mlicpp.py:107-176 (forward), 220-277 (compress), 309-366 (decompress)
@@ -760,7 +768,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.sym = d_sym + (int64_t)phase_id * L().B * n_per;
           Q.idx = d_idx + (int64_t)phase_id * L().B * n_per;
         }
-        timed(PCAT_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); });
+        timed(PCAT_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); }, "quant_phase");
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
       lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
@@ -786,7 +794,7 @@ void Model::eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym) {
   P.H = z.H;
   P.W = z.W;
   P.B = L().B;
-  timed(PCAT_ELEM, 0.0, 12.0 * L().B * z.C * z.H * z.W, [&] { eb_forward(P, L().st); });
+  timed(PCAT_ELEM, 0.0, 12.0 * L().B * z.C * z.H * z.W, [&] { eb_forward(P, L().st); }, "entropy_bottleneck");
 }
 
 template <class F>
@@ -1022,10 +1030,14 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   HIP_OK(hipMemcpyAsync(hs, d_sym, ny * 4, hipMemcpyDeviceToHost, l.st));
   HIP_OK(hipMemcpyAsync(hi, d_idx, ny * 4, hipMemcpyDeviceToHost, l.st));
   HIP_OK(hipMemcpyAsync(hzs, d_zsym, nz * 4, hipMemcpyDeviceToHost, l.st));
-  HIP_OK(hipStreamSynchronize(l.st));
+  {
+    HostStats::Scope w{hstats_.wait_ns};
+    HIP_OK(hipStreamSynchronize(l.st));
+  }
   l.enc.assign(B, EncodedImage{});
   const int64_t zper = (int64_t)cfg_.N * hz * wz;
   auto work = [&](int b) {
+    HostStats::Scope e{hstats_.enc_ns};
     // y: phases in order, this image's part of each ([phase][B][n_per] on device)
     std::vector<int32_t> s((size_t)nph * n_per), ix((size_t)nph * n_per);
     for (int k = 0; k < nph; ++k) {
@@ -1088,7 +1100,7 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
       d.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
     }
   }
-  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx);
+  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_);
   const int32_t* hz_sym = l.h_sym;
   planned(B, nullptr, [&] {
     int32_t* d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(B * zper));

@@ -1,6 +1,8 @@
 // MLIC++ model executor: the reference's module graph (models/mlicpp.py, mlicpp_small_decoder.py,
 // mlicpp_vbr.py) driven natively over the HIP kernels, on one stream, with a per-handle arena.
 #pragma once
+#include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <string>
@@ -72,6 +74,18 @@ struct EncodedImage {
 
 class PhaseDecoder;
 
+// host-side time accounting (summed over threads): entropy coding and waits on the GPU
+struct HostStats {
+  std::atomic<int64_t> enc_ns{0}, dec_ns{0}, wait_ns{0};
+  struct Scope {
+    std::atomic<int64_t>& acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~Scope() {
+      acc += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
+  };
+};
+
 // Per-call execution state.  A Model owns several lanes so that a batch can be split over host
 // threads, each driving its own HIP stream: one lane's host entropy coding overlaps another
 // lane's kernels (weights and entropy tables are shared, read-only).
@@ -107,6 +121,7 @@ class Model {
         const int* ndims, hipStream_t st);
   ~Model();
   const Cfg& cfg() const { return cfg_; }
+  HostStats& host_stats() { return hstats_; }
 
   // forward(): x [B,3,H,W] -> x_hat, y_lik [B,M,H/16,W/16], z_lik [B,N,H/64,W/64] (any may be null)
   void forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
@@ -149,6 +164,7 @@ class Model {
   std::vector<std::unique_ptr<Lane>> lanes_;
   int nlanes_ = 2;
   int precision_ = PREC_F16X3_V2;
+  HostStats hstats_;
   bool prof_ = false;
   static thread_local Lane* tl_lane_;
   Lane& L() const { return *tl_lane_; }

@@ -20,10 +20,6 @@ constexpr int PRECISION = 16;
 constexpr int BYPASS_PRECISION = 4;
 constexpr int MAX_BYPASS_VAL = (1 << BYPASS_PRECISION) - 1;
 
-struct Sym {  // a coded symbol: table*stride + value (regular) or the 4-bit bypass value | flag
-  uint32_t v;
-};
-constexpr uint32_t BYPASS_FLAG = 0x80000000u;
 
 inline uint64_t mulhi64(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
 
@@ -75,44 +71,40 @@ inline void enc_put_bits(uint64_t& x, uint32_t*& ptr, uint32_t val, uint32_t nbi
 
 std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t) {
   if (t.enc.empty()) throw std::runtime_error("rans: tables not prepared");
-  std::vector<Sym> syms;
-  syms.reserve((size_t)n + 16);
-  for (int64_t i = 0; i < n; ++i) {
-    const int32_t ci = indexes[i];
-    if (ci < 0 || ci >= t.n) throw std::runtime_error("rans: cdf index out of range");
-    const int32_t max_value = t.length[ci] - 2;
-    int32_t value = symbols[i] - t.offset[ci];
-    uint32_t raw = 0;
-    if (value < 0) {
-      raw = (uint32_t)(-2 * (int64_t)value - 1);
-      value = max_value;
-    } else if (value >= max_value) {
-      raw = (uint32_t)(2 * ((int64_t)value - max_value));
-      value = max_value;
-    }
-    syms.push_back({(uint32_t)(ci * t.stride + value)});
-    if (value == max_value) {
-      int32_t nb = 0;
-      while (nb < 8 && (raw >> (nb * BYPASS_PRECISION)) != 0) ++nb;
-      int32_t v = nb;
-      while (v >= MAX_BYPASS_VAL) {
-        syms.push_back({BYPASS_FLAG | (uint32_t)MAX_BYPASS_VAL});
-        v -= MAX_BYPASS_VAL;
-      }
-      syms.push_back({BYPASS_FLAG | (uint32_t)v});
-      for (int32_t j = 0; j < nb; ++j)
-        syms.push_back({BYPASS_FLAG | ((raw >> (j * BYPASS_PRECISION)) & MAX_BYPASS_VAL)});
-    }
-  }
-  std::vector<uint32_t> out(syms.size() + 4, 0xCCCCCCCCu);
+  // One reverse pass.  compressai pushes, per symbol: the symbol (value clamped to max_value) and,
+  // if escaped, the bypass length nb (< 15 for 32-bit values) and nb 4-bit chunks of the raw
+  // value; the coder consumes that stream LIFO, so walking symbols backwards we emit the raw
+  // chunks (last first), then nb, then the symbol.  Each emit writes at most one 32-bit word.
+  std::vector<uint32_t> out((size_t)n + 64, 0u);
   uint32_t* end = out.data() + out.size();
   uint32_t* ptr = end;
   uint64_t x = RANS64_L;
   const EncSym* es = t.enc.data();
-  for (size_t k = syms.size(); k-- > 0;) {
-    const uint32_t v = syms[k].v;
-    if (!(v & BYPASS_FLAG)) enc_put_sym(x, ptr, es[v]);
-    else enc_put_bits(x, ptr, v & ~BYPASS_FLAG, BYPASS_PRECISION);
+  const int32_t* len = t.length.data();
+  const int32_t* off = t.offset.data();
+  const int stride = t.stride;
+  for (int64_t i = n; i-- > 0;) {
+    if ((size_t)(ptr - out.data()) < 16) {  // grow: keep the written tail at the end of a larger buffer
+      const size_t used = (size_t)(end - ptr);
+      std::vector<uint32_t> bigger(out.size() * 2 + 64, 0u);
+      std::memcpy(bigger.data() + bigger.size() - used, ptr, used * 4);
+      out.swap(bigger);
+      end = out.data() + out.size();
+      ptr = end - used;
+    }
+    const int32_t ci = indexes[i];
+    if ((uint32_t)ci >= (uint32_t)t.n) throw std::runtime_error("rans: cdf index out of range");
+    const int32_t max_value = len[ci] - 2;
+    int32_t value = symbols[i] - off[ci];
+    if (value < 0 || value >= max_value) {
+      const uint32_t raw = value < 0 ? (uint32_t)(-2 * (int64_t)value - 1) : (uint32_t)(2 * ((int64_t)value - max_value));
+      int32_t nb = 0;
+      while (nb < 8 && (raw >> (nb * BYPASS_PRECISION)) != 0) ++nb;
+      for (int32_t j = nb; j-- > 0;) enc_put_bits(x, ptr, (raw >> (j * BYPASS_PRECISION)) & MAX_BYPASS_VAL, BYPASS_PRECISION);
+      enc_put_bits(x, ptr, (uint32_t)nb, BYPASS_PRECISION);
+      value = max_value;
+    }
+    enc_put_sym(x, ptr, es[(int64_t)ci * stride + value]);
   }
   ptr -= 2;  // flush
   ptr[0] = (uint32_t)(x >> 0);
