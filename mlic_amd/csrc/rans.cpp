@@ -128,34 +128,43 @@ uint32_t RansDecoderState::get_word() {
 
 void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables& t, int32_t* out) {
   constexpr uint64_t mask = (1ull << PRECISION) - 1;
+  constexpr int SHIFT = PRECISION - CdfTables::LUT_BITS;
+  const int32_t* len = t.length.data();
+  const int32_t* off = t.offset.data();
+  const uint64_t* lut = t.lut.data();
+  const int32_t* cdfs = t.cdf.data();
+  const int stride = t.stride;
+  uint64_t state = state_;
   for (int64_t i = 0; i < n; ++i) {
     const int32_t ci = indexes[i];
-    if (ci < 0 || ci >= t.n) throw std::runtime_error("rans: cdf index out of range");
-    const int32_t* cdf = t.cdf.data() + (int64_t)ci * t.stride;
-    const int32_t len = t.length[ci];
-    const int32_t max_value = len - 2;
-    const uint32_t cum = (uint32_t)(state_ & mask);
-    // s = (first entry > cum) - 1; the bucket table gives a start at or below s (cdf strictly increasing)
-    int32_t s;
-    if (!t.lut.empty()) {
-      s = t.lut[(size_t)ci * (1u << CdfTables::LUT_BITS) + (cum >> (PRECISION - CdfTables::LUT_BITS))];
-      while (s < len - 1 && (uint32_t)cdf[s + 1] <= cum) ++s;
+    if ((uint32_t)ci >= (uint32_t)t.n) throw std::runtime_error("rans: cdf index out of range");
+    const uint32_t cum = (uint32_t)(state & mask);
+    const uint64_t e = lut[((size_t)ci << CdfTables::LUT_BITS) + (cum >> SHIFT)];
+    int32_t s = (int32_t)(e & 0xffff);
+    uint32_t start, freq;
+    if (e >> 63) {
+      start = (uint32_t)(e >> 16) & 0xffff;
+      freq = (uint32_t)(e >> 32) & 0x1ffff;
     } else {
-      s = (int32_t)(std::upper_bound(cdf, cdf + len, (int32_t)cum) - cdf) - 1;
+      const int32_t* cdf = cdfs + (int64_t)ci * stride;
+      const int32_t l = len[ci];
+      while (s < l - 1 && (uint32_t)cdf[s + 1] <= cum) ++s;
+      start = (uint32_t)cdf[s];
+      freq = (uint32_t)(cdf[s + 1] - cdf[s]);
     }
-    if (s < 0 || s > max_value) throw std::runtime_error("rans: corrupt stream");
-    const uint32_t start = (uint32_t)cdf[s], freq = (uint32_t)(cdf[s + 1] - cdf[s]);
-    uint64_t x = freq * (state_ >> PRECISION) + (state_ & mask) - start;
+    const int32_t max_value = len[ci] - 2;
+    if (s > max_value) throw std::runtime_error("rans: corrupt stream");
+    uint64_t x = freq * (state >> PRECISION) + cum - start;
     if (x < RANS64_L) x = (x << 32) | get_word();
-    state_ = x;
+    state = x;
     int32_t value = s;
     if (value == max_value) {
       auto get_bits = [&](uint32_t nb) {
-        uint64_t y = state_;
+        uint64_t y = state;
         const uint32_t v = (uint32_t)(y & ((1u << nb) - 1));
         y >>= nb;
         if (y < RANS64_L) y = (y << 32) | get_word();
-        state_ = y;
+        state = y;
         return v;
       };
       int32_t v = (int32_t)get_bits(BYPASS_PRECISION);
@@ -171,8 +180,9 @@ void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables
       if (raw & 1) value = -value - 1;
       else value += max_value;
     }
-    out[i] = value + t.offset[ci];
+    out[i] = value + off[ci];
   }
+  state_ = state;
 }
 
 void CdfTables::prepare() {
@@ -189,10 +199,14 @@ void CdfTables::prepare() {
       enc[(size_t)k * stride + v] = make_enc_sym((uint32_t)c[v], (uint32_t)(c[v + 1] - c[v]));
     }
     int s = 0;
+    const uint32_t width = 1u << (PRECISION - LUT_BITS);
     for (size_t b = 0; b < L; ++b) {
       const uint32_t lo = (uint32_t)(b << (PRECISION - LUT_BITS));
       while (s < len - 2 && (uint32_t)c[s + 1] <= lo) ++s;
-      lut[(size_t)k * L + b] = (uint16_t)s;
+      uint64_t e = (uint64_t)s;
+      if ((uint32_t)c[s + 1] >= lo + width)  // the whole bucket lies inside symbol s
+        e |= (1ull << 63) | ((uint64_t)(uint32_t)c[s] << 16) | ((uint64_t)(uint32_t)(c[s + 1] - c[s]) << 32);
+      lut[(size_t)k * L + b] = e;
     }
   }
 }

@@ -24,7 +24,9 @@ struct CdfTables {
   // derived (prepare()): per-symbol encoder records and a 2^LUT_BITS decode bucket table
   static constexpr int LUT_BITS = 10;
   std::vector<EncSym> enc;       // [n][stride]
-  std::vector<uint16_t> lut;     // [n][1 << LUT_BITS]: first symbol s with cdf[s+1] > bucket start
+  // [n][1 << LUT_BITS] decode buckets: bit 63 set => the whole bucket decodes to one symbol and the
+  // entry holds (symbol | start << 16 | freq << 32); else the low 16 bits are the first candidate
+  std::vector<uint64_t> lut;
   void prepare();
 };
 
