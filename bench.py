@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 # the split-fp16 kernels issue 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of
 # fp32-equivalent work; the VALU conv kernels run exact fp32 FMAs (157.3 TF with packed FMA)
 def kernel_peak(name: str):
-    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident")):
+    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv3x3_halo")):
         return 2500.0 / 3, "3 x v_mfma_f32_32x32x16_f16 per fp32 product (split-fp16)"
     if name.startswith("conv_mfma"):
         return 157.3, "v_mfma_f32_32x32x2_f32"
@@ -130,9 +130,17 @@ def main():
     B, H, W = a.batch, a.height, a.width
     x = torch.cat([synthetic.synth_image(H, W, 1000 * rank + i) for i in range(B)]).to(dev)
 
+    split = {"compress": 0.0, "decompress": 0.0}
+
     def step():
+        t_a = time.perf_counter()
         c = net.compress(x)
+        torch.cuda.synchronize()
+        t_b = time.perf_counter()
         d = net.decompress(c["strings"], c["shape"])
+        torch.cuda.synchronize()
+        split["compress"] += t_b - t_a
+        split["decompress"] += time.perf_counter() - t_b
         return c, d
 
     for _ in range(a.warmup):
@@ -143,6 +151,7 @@ def main():
     torch.cuda.synchronize()
     hs = [C.c_double() for _ in range(3)]
     _lib.call("mlic_host_stats", net._handle, *[C.byref(v) for v in hs], 1)
+    split["compress"] = split["decompress"] = 0.0
     t0 = time.perf_counter()
     for _ in range(a.steps):
         c, d = step()
@@ -153,6 +162,7 @@ def main():
     elapsed = time.perf_counter() - t0
     _lib.call("mlic_host_stats", net._handle, *[C.byref(v) for v in hs], 1)
     host = {k: round(v.value / a.steps, 2) for k, v in zip(("rans_encode", "rans_decode", "gpu_wait"), hs)}
+    wall_split = {k: round(1000 * v / a.steps, 2) for k, v in split.items()}
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -251,6 +261,7 @@ def main():
             "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
             "host_thread_ms_per_step": host,
+            "wall_ms_per_step": wall_split,
             "lanes": a.lanes,
             "quality": {"bpp_file_mean": round(float(rec[:, 1].mean()), 5),
                         "psnr_u8_mean": round(float(rec[:, 2].mean()), 4), "images": int(rec.shape[0])},

@@ -86,7 +86,7 @@ int mlic_profile_category_name(int cat, char* buf, size_t cap);
 
 /* kernel-level entry points (bit-exact tests, micro-benchmarks) */
 /* one conv layer with a given kernel family: impl -1 = the model's choice (precision 2), 0 fp32 MFMA,
- * 1 f16x3, 2 f16x3 v2, 3 resident-weight 1x1, 4 narrow 3x3, 5 small-Cin 1x1.  w is torch layout
+ * 1 f16x3, 2 f16x3 v2, 3 resident-weight 1x1, 4 narrow 3x3, 5 small-Cin 1x1, 6 halo-tiled 3x3.  w is torch layout
  * [Cout][Cin][K][K]; pad = K/2; epi = Epi flags of common.h (aux for GDN, res for residual).
  * Synchronous on `stream`. */
 int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,

@@ -149,7 +149,7 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
 
 int mlic_set_precision(mlic_model* m, int precision) {
   return guard([&] {
-    MLIC_CHECK(precision >= 0 && precision <= 3, "precision must be 0 (f32), 1, 2 or 3 (f16x3 tiles v1/v2/v3)");
+    MLIC_CHECK(precision >= PREC_F32 && precision <= PREC_F16X3_V2, "precision must be 0 (f32), 1 or 2 (f16x3)");
     m->impl->set_precision(precision);
   });
 }
@@ -223,7 +223,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     P.out_cs = (int64_t)Ho * Wo;
     P.epi = shuffle ? EPI_SHUFFLE : 0;
     const ConvWeights cw{wp, wh, wl, cin_pad};
-    const int which = impl == 3 ? conv_select(P, cw, 2) : impl == 7 ? conv_select(P, cw, 3) : impl;  // 3/7 = model choice at precision 2/3
+    const int which = impl == 3 ? conv_select(P, cw, 2) : impl;  // 3 = what the model runs (precision 2)
     auto launch = [&] { conv_run(which, P, cw, nullptr); };
     launch();
     HIP_OK(hipDeviceSynchronize());
@@ -304,6 +304,7 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
     if (which == CONV_NARROW) MLIC_CHECK(conv_narrow_ok(P), "narrow: unsupported shape");
     if (which == CONV_SMALLCIN) MLIC_CHECK(conv_smallcin_ok(P), "smallcin: unsupported shape");
+    if (which == CONV_HALO) MLIC_CHECK(conv_halo_ok(P, cin_pad), "halo: unsupported shape");
     conv_run(which, P, cw, st);
     HIP_OK(hipFreeAsync(wp, st));
     HIP_OK(hipFreeAsync(wh, st));

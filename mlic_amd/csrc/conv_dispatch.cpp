@@ -9,10 +9,10 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (conv_narrow_ok(P)) return CONV_NARROW;      // exact fp32 VALU, all precisions
   if (precision == 0 || !w.wh) return CONV_F32;
   if (precision == 1) return CONV_X3;
-  const int tiles = precision >= 3 ? CONV_X3V3 : CONV_X3V2;
   // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
   if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
-  return tiles;
+  if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && conv_halo_ok(P, w.cin_pad)) return CONV_HALO;
+  return CONV_X3V2;
 }
 
 int conv_prof_cat(int impl, const ConvParams& P) {
@@ -20,9 +20,9 @@ int conv_prof_cat(int impl, const ConvParams& P) {
     case CONV_F32: return PCAT_CONV_F32 + conv_variant(P);
     case CONV_X3: return PCAT_CONV_X3 + conv_f16x3_variant(P);
     case CONV_X3V2: return PCAT_CONV_X3V2 + std::min(conv_x3v2_variant(P), 2);
-    case CONV_X3V3: return PCAT_CONV_X3V3 + std::min(conv_x3v2_variant(P), 2);
     case CONV_PW: return PCAT_CONV_PW;
     case CONV_NARROW: return PCAT_CONV_NARROW;
+    case CONV_HALO: return PCAT_CONV_HALO;
     default: return PCAT_CONV_SMALLCIN;
   }
 }
@@ -32,10 +32,10 @@ void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t s
     case CONV_F32: conv_forward(P, st); break;
     case CONV_X3: conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, st); break;
     case CONV_X3V2: conv_x3v2_forward(P, w.wh, w.wl, w.cin_pad, st); break;
-    case CONV_X3V3: conv_x3v3_forward(P, w.wh, w.wl, w.cin_pad, st); break;
     case CONV_PW: pw_resident_forward(P, w.wh, w.wl, w.cin_pad, st); break;
     case CONV_NARROW: conv_narrow_forward(P, st); break;
     case CONV_SMALLCIN: conv_smallcin_forward(P, st); break;
+    case CONV_HALO: conv_halo_forward(P, w.wh, w.wl, w.cin_pad, st); break;
     default: throw Error("mlic: unknown conv implementation " + std::to_string(impl));
   }
 }
@@ -45,9 +45,9 @@ const char* prof_cat_name(int cat) {
       "conv_mfma_kernel<64,64>",     "conv_mfma_kernel<64,128>",  "conv_mfma_kernel<128,64>",
       "conv_mfma_kernel<128,128>",   "conv_f16x3_kernel<32,256>", "conv_f16x3_kernel<64,128>",
       "conv_f16x3_kernel<128,64>",   "conv_f16x3_kernel<128,128>", "conv_x3v2_kernel<64,128>",
-      "conv_x3v2_kernel<128,256>",   "conv_x3v2_kernel<128,128>", "conv_x3v3_kernel<64,128>",
-      "conv_x3v3_kernel<128,256>",   "conv_x3v3_kernel<128,128>", "pw_resident_kernel",
-      "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "dw3x3_kernel",
+      "conv_x3v2_kernel<128,256>",   "conv_x3v2_kernel<128,128>", "pw_resident_kernel",
+      "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "conv3x3_halo_kernel",
+      "dw3x3_kernel",
       "local_attn_kernel",           "linear_attention",          "elementwise"};
   return (cat >= 0 && cat < PCAT_COUNT) ? names[cat] : "";
 }

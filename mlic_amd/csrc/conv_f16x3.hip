@@ -516,270 +516,6 @@ void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// v3: the v2 tiles with two register stages of prefetch (see the main loop)
-template <int BM, int BN>
-__global__ __launch_bounds__(XB_THREADS, 2) void conv_x3v3_kernel(ConvParams P, const _Float16* __restrict__ wh,
-                                                                const _Float16* __restrict__ wl, int cin_pad) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_CHUNKS = BM * XB_K / 8 / XB_THREADS;
-  constexpr int QN = BN / 4;                 // pixel quads per k row
-  constexpr int RPT = XB_K * QN / XB_THREADS;  // k rows staged per thread
-  static_assert(A_CHUNKS >= 1 && RPT >= 1 && RPT <= 16, "tile");
-  constexpr int APITCH = XB_PITCH;           // halves
-  constexpr int BPITCH = BN + 32;            // halves
-  constexpr int A_SZ = BM * APITCH, B_SZ = XB_K * BPITCH;
-  constexpr int BUF = 2 * A_SZ + 2 * B_SZ;
-  __shared__ __attribute__((aligned(16))) _Float16 sm[2 * BUF];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nct = gridDim.x, npt = gridDim.y, nblk = nct * npt;
-  const int bid = blockIdx.y * nct + blockIdx.x;
-  int logical = bid;
-  if (nblk >= 16) {
-    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-    logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int ct = logical % nct, pt = logical / nct;
-  const int b = blockIdx.z;
-  const int co0 = ct * BM, p0 = pt * BN;
-  const int HWo = P.Ho * P.Wo;
-  const int64_t HWi = (int64_t)P.H * P.W;
-  const int KK = P.K * P.K;
-
-  const int pq = tid % QN, kr0 = (tid / QN) * RPT;
-  const int n0 = 4 * pq;
-  int ohs[4], ows[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int p = min(p0 + n0 + q, HWo - 1);
-    ohs[q] = p / P.Wo;
-    ows[q] = p - ohs[q] * P.Wo;
-  }
-  const bool fast1x1 = P.K == 1 && P.stride == 1 && P.pad == 0 && (HWo & 3) == 0;
-  const bool quad_ok = p0 + n0 + 3 < HWo;
-
-  const int nck = cin_pad / XB_K;
-  const int ntile = KK * nck;
-  const bool square = (P.epi & EPI_SQUARE_IN) != 0;
-
-  struct Stage {
-    uint4 ra_h[A_CHUNKS], ra_l[A_CHUNKS];
-    float rb[RPT][4];
-  };
-  Stage S0, S1;
-
-  auto load_tile = [&](Stage& S, int t) {
-    auto& ra_h = S.ra_h;
-    auto& ra_l = S.ra_l;
-    auto& rb = S.rb;
-    const int tap = t / nck;
-    const int c0 = (t - tap * nck) * XB_K;
-#pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) {
-      const int id = tid + i * XB_THREADS;
-      const int row = id >> 2, qq = id & 3;
-      const int co = co0 + row;
-      if (co < P.Cout) {
-        const int64_t off = ((int64_t)co * KK + tap) * cin_pad + c0 + 8 * qq;
-        ra_h[i] = *reinterpret_cast<const uint4*>(wh + off);
-        ra_l[i] = *reinterpret_cast<const uint4*>(wl + off);
-      } else {
-        ra_h[i] = make_uint4(0, 0, 0, 0);
-        ra_l[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
-    // rows kr0 .. kr0 + RPT of this tile lie inside one 16-channel group => one segment
-    const int cg = c0 + kr0;
-    int s = 0, segc0 = 0;
-    while (s + 1 < P.nseg && cg >= segc0 + P.seg[s].C) { segc0 += P.seg[s].C; ++s; }
-    const Seg sg = P.seg[s];
-    const int cl = cg - segc0;
-    const float* plane = sg.p + (int64_t)b * sg.bs + (int64_t)cl * HWi;
-    if (fast1x1 && quad_ok) {
-#pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const bool ok = (cg + r) < P.Cin && (cl + r) < sg.C;
-        float4 v = ok ? *reinterpret_cast<const float4*>(plane + (int64_t)r * HWi + p0 + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        rb[r][0] = v.x; rb[r][1] = v.y; rb[r][2] = v.z; rb[r][3] = v.w;
-      }
-    } else {
-      const int ky = tap / P.K, kx = tap - ky * P.K;
-      int off[4];
-      bool inb[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ih = ohs[q] * P.stride + ky - P.pad, iw = ows[q] * P.stride + kx - P.pad;
-        inb[q] = (p0 + n0 + q) < HWo && ih >= 0 && ih < P.H && iw >= 0 && iw < P.W;
-        off[q] = ih * P.W + iw;
-      }
-#pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const bool ok = (cg + r) < P.Cin && (cl + r) < sg.C;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rb[r][q] = (ok && inb[q]) ? plane[(int64_t)r * HWi + off[q]] : 0.0f;
-      }
-    }
-    if (square) {
-#pragma unroll
-      for (int r = 0; r < RPT; ++r)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rb[r][q] *= rb[r][q];
-    }
-  };
-
-  auto store_tile = [&](const Stage& S, int buf) {
-    const auto& ra_h = S.ra_h;
-    const auto& ra_l = S.ra_l;
-    const auto& rb = S.rb;
-    _Float16* base = sm + buf * BUF;
-#pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) {
-      const int id = tid + i * XB_THREADS;
-      const int row = id >> 2, qq = id & 3;
-      *reinterpret_cast<uint4*>(base + row * APITCH + 8 * qq) = ra_h[i];
-      *reinterpret_cast<uint4*>(base + A_SZ + row * APITCH + 8 * qq) = ra_l[i];
-    }
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-      half4 h, l;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const _Float16 hv = (_Float16)rb[r][q];
-        h[q] = hv;
-        l[q] = (_Float16)(rb[r][q] - (float)hv);
-      }
-      *reinterpret_cast<half4*>(base + 2 * A_SZ + (kr0 + r) * BPITCH + n0) = h;
-      *reinterpret_cast<half4*>(base + 2 * A_SZ + B_SZ + (kr0 + r) * BPITCH + n0) = l;
-    }
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-  const int l32 = lane & 31;
-  const int kh = (lane >> 5) * 8;
-  // tr-read addressing: 16-lane group g, lane 4q+p supplies row q, columns 4p..4p+3
-  const int g = lane >> 4, li = lane & 15;
-  const int trow = kh + (li >> 2);
-  const int tcol = (g & 1) * 16 + 4 * (li & 3);
-  auto compute = [&](int cur) {
-    const _Float16* base = sm + cur * BUF;
-    const _Float16* Bh = base + 2 * A_SZ;
-    const _Float16* Bl = base + 2 * A_SZ + B_SZ;
-#pragma unroll
-    for (int ks = 0; ks < XB_K; ks += 16) {
-      half8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 32 + l32;
-        ah[i] = *reinterpret_cast<const half8*>(base + row * APITCH + ks + kh);
-        al[i] = *reinterpret_cast<const half8*>(base + A_SZ + row * APITCH + ks + kh);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * WN + j * 32 + tcol;
-        const int o0 = (ks + trow) * BPITCH + col;
-        bh[j] = tr_read8(Bh + o0, Bh + o0 + 4 * BPITCH);
-        bl[j] = tr_read8(Bl + o0, Bl + o0 + 4 * BPITCH);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    }
-  };
-
-  // two register stages in flight: the loads of tile t+2 are issued while tile t is computed and
-  // written to LDS only after tile t+1 has been computed, so each load has two MFMA phases to land;
-  // one barrier per K-step (the LDS buffer being written was last read before that barrier)
-  load_tile(S0, 0);
-  store_tile(S0, 0);
-  if (ntile > 1) load_tile(S1, 1);
-  if (ntile > 2) load_tile(S0, 2);
-  __syncthreads();
-  for (int t = 0; t < ntile; t += 2) {
-    compute(0);
-    if (t + 1 < ntile) store_tile(S1, 1);
-    __syncthreads();
-    if (t + 1 >= ntile) break;
-    if (t + 3 < ntile) load_tile(S1, t + 3);
-    compute(1);
-    if (t + 2 < ntile) store_tile(S0, 0);
-    __syncthreads();
-    if (t + 4 < ntile) load_tile(S0, t + 4);
-  }
-
-  const int epi = P.epi;
-  const int khalf = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int p = p0 + wn * WN + j * 32 + l32;
-      if (p >= HWo) continue;
-      const int oh = p / P.Wo, ow = p - (p / P.Wo) * P.Wo;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = co0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-        if (co >= P.Cout) continue;
-        float v = acc[i][j][r];
-        if (P.bias) v += P.bias[co];
-        if (epi & EPI_GELU) v = gelu_erf(v);
-        if (epi & (EPI_GDN | EPI_IGDN)) {
-          const float x = P.aux[(int64_t)b * P.aux_bs + (int64_t)co * HWo + p];
-          v = (epi & EPI_GDN) ? x * (1.0f / sqrtf(v)) : x * sqrtf(v);
-        }
-        if (epi & EPI_TANH_HALF) v = 0.5f * tanhf(v);
-        if (epi & EPI_MASK_ANCHOR) v = is_anchor(oh, ow) ? v : 0.0f;
-        if (epi & EPI_MASK_NONANCHOR) v = is_anchor(oh, ow) ? 0.0f : v;
-        int64_t off;
-        if (epi & EPI_SHUFFLE) {
-          const int oc = co >> 2;
-          const int y2 = 2 * oh + ((co >> 1) & 1), x2 = 2 * ow + (co & 1);
-          off = (int64_t)oc * P.out_cs + (int64_t)y2 * (2 * P.Wo) + x2;
-        } else {
-          off = (int64_t)co * P.out_cs + p;
-        }
-        if (epi & EPI_RES) v = P.res[(int64_t)b * P.res_bs + off] + v;
-        P.out[(int64_t)b * P.out_bs + off] = v;
-      }
-    }
-  }
-}
-
-template <int BM, int BN>
-static void launch_v3(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
-  const int HWo = P.Ho * P.Wo;
-  dim3 grid((P.Cout + BM - 1) / BM, (HWo + BN - 1) / BN, P.B);
-  hipLaunchKernelGGL((conv_x3v3_kernel<BM, BN>), grid, dim3(XB_THREADS), 0, st, P, wh, wl, cin_pad);
-  HIP_OK(hipGetLastError());
-}
-
-void conv_x3v3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
-  MLIC_CHECK(cin_pad % XB_K == 0 && cin_pad >= P.Cin, "f16x3: padded Cin");
-  for (int s = 0; s + 1 < P.nseg; ++s) MLIC_CHECK(P.seg[s].C % 16 == 0, "f16x3: segments must be 16-aligned");
-  switch (conv_x3v2_variant(P)) {
-    case 0: launch_v3<64, 128>(P, wh, wl, cin_pad, st); break;
-    case 1: launch_v3<128, 256>(P, wh, wl, cin_pad, st); break;
-    default: launch_v3<128, 128>(P, wh, wl, cin_pad, st); break;
-  }
-}
-
 // weights [Cout][Cin][K][K] fp32 -> hi/lo fp16 [Cout][K*K][cin_pad] (zero padded)
 __global__ void split_weights_kernel(const float* __restrict__ w, _Float16* __restrict__ wh, _Float16* __restrict__ wl,
                                      int Cout, int Cin, int KK, int cin_pad) {

@@ -17,7 +17,6 @@ int conv_f16x3_variant(const ConvParams& P);
 void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 int conv_x3v2_variant(const ConvParams& P);
 void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
-void conv_x3v3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad,
                    hipStream_t st);
 
@@ -26,12 +25,14 @@ bool pw_resident_ok(const ConvParams& P, int cin_pad);
 void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 bool conv_narrow_ok(const ConvParams& P);
 void conv_narrow_forward(const ConvParams& P, hipStream_t st);
+bool conv_halo_ok(const ConvParams& P, int cin_pad);
+void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 bool conv_smallcin_ok(const ConvParams& P);
 void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 
 // kernel-family selection (conv_dispatch.cpp)
 enum ConvImpl : int {
-  CONV_F32 = 0, CONV_X3 = 1, CONV_X3V2 = 2, CONV_PW = 3, CONV_NARROW = 4, CONV_SMALLCIN = 5, CONV_X3V3 = 6
+  CONV_F32 = 0, CONV_X3 = 1, CONV_X3V2 = 2, CONV_PW = 3, CONV_NARROW = 4, CONV_SMALLCIN = 5, CONV_HALO = 6
 };
 struct ConvWeights {
   const float* wpk;  // fp32 packed [K*K][Cin][Cout] (in ConvParams too)
@@ -47,15 +48,15 @@ enum ProfCat : int {
   PCAT_CONV_F32 = 0,     // 0..3  conv_mfma_kernel tiles (conv_variant)
   PCAT_CONV_X3 = 4,      // 4..7  conv_f16x3_kernel tiles (conv_f16x3_variant)
   PCAT_CONV_X3V2 = 8,    // 8..10 conv_x3v2_kernel tiles
-  PCAT_CONV_X3V3 = 11,   // 11..13 conv_x3v3_kernel tiles
-  PCAT_CONV_PW = 14,
-  PCAT_CONV_NARROW = 15,
-  PCAT_CONV_SMALLCIN = 16,
-  PCAT_DW = 17,
-  PCAT_LOCAL = 18,
-  PCAT_LINATT = 19,
-  PCAT_ELEM = 20,
-  PCAT_COUNT = 21
+  PCAT_CONV_PW = 11,
+  PCAT_CONV_NARROW = 12,
+  PCAT_CONV_SMALLCIN = 13,
+  PCAT_CONV_HALO = 14,
+  PCAT_DW = 15,
+  PCAT_LOCAL = 16,
+  PCAT_LINATT = 17,
+  PCAT_ELEM = 18,
+  PCAT_COUNT = 19
 };
 int conv_prof_cat(int impl, const ConvParams& P);
 const char* prof_cat_name(int cat);

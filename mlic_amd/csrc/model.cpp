@@ -2,6 +2,8 @@
 // the HIP kernels (conv_mfma.hip, kernels.hip), this file only wires views, weights and phases.
 #include "model.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -202,7 +204,16 @@ thread_local Lane* Model::tl_lane_ = nullptr;
 Lane& Model::lane(int i) {
   while ((int)lanes_.size() <= i) {
     auto l = std::make_unique<Lane>();
-    HIP_OK(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
+    // staggered priorities (lane 0 highest): symmetric lanes would reach their host entropy-coding
+    // phases together and leave the GPU idle; with priorities they drift apart and each lane's host
+    // coding overlaps the lower-priority lanes' kernels.  MLIC_LANE_PRIORITY=0 disables.
+    int least = 0, greatest = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* e = std::getenv("MLIC_LANE_PRIORITY");
+    const bool stagger = !(e && std::atoi(e) == 0);
+    const int idx = (int)lanes_.size();
+    const int prio = stagger ? std::min(least, greatest + idx) : least;
+    HIP_OK(hipStreamCreateWithPriority(&l->st, hipStreamNonBlocking, prio));
     l->own_stream = true;
     l->prof = prof_;
     lanes_.push_back(std::move(l));

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 GELU, GDN, IGDN, RES, SHUFFLE, SQUARE = 1, 2, 4, 64, 128, 256
-F32, X3, X3V2, PW, NARROW, SMALLCIN, X3V3, AUTO = 0, 1, 2, 3, 4, 5, 6, -1
+F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, AUTO = 0, 1, 2, 3, 4, 5, 6, -1
 
 
 def reference(x, w, b, stride, epi, res):
@@ -86,7 +86,7 @@ def test_smallcin(stride):
     check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride))
 
 
-@pytest.mark.parametrize("impl", [F32, X3, X3V2, X3V3])
+@pytest.mark.parametrize("impl", [F32, X3, X3V2])
 @pytest.mark.parametrize("shape", [
     (2, 192, 768, 24, 40, 3, 1, SHUFFLE | GELU),  # subpel conv
     (2, 192, 192, 33, 47, 1, 1, GDN | SQUARE),     # GDN on the generic tiles
@@ -99,6 +99,18 @@ def test_smallcin(stride):
 def test_generic_tiles(impl, shape):
     B, cin, cout, H, W, K, s, epi = shape
     check(*run(impl, B, cin, cout, H, W, K, stride=s, epi=epi))
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 192, 768, 24, 64, SHUFFLE | GELU),   # g_s subpel conv, 2 x 3 tiles
+    (1, 192, 768, 19, 45, SHUFFLE),          # ragged tiles at every edge
+    (2, 96, 192, 16, 32, GELU | RES),        # Cout not a multiple of 128, residual
+    (1, 160, 96, 9, 40, 0),                  # Cin 160 (5 chunks), Cout < 128
+    (1, 100, 64, 8, 32, GDN | SQUARE),       # Cin not a multiple of 32 (zero-padded chunk)
+])
+def test_halo(shape):
+    B, cin, cout, H, W, epi = shape
+    check(*run(HALO, B, cin, cout, H, W, 3, epi=epi))
 
 
 def test_auto_matches_selected_family():
