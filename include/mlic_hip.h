@@ -98,6 +98,9 @@ int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias,
 int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
                     double* ms_per, double* tflops);
 int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */
+/* LocalContext window attention: qkv [B][3C][H*W] -> out [B][25C][H*W]; impl 0 = VALU, 1 = MFMA */
+int mlic_local_attn_run(void* stream, int impl, const float* qkv, const float* rel_table, const int32_t* rel_index,
+                        float* out, int C, int H, int W, int B, float scale);
 int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);
 int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out);
 

@@ -1,0 +1,174 @@
+// LocalContext 5x5 window attention (context.py:75-107) on the split-fp16 MFMA pipe.
+//
+// For every latent pixel p and head, the 25 cells of its 5x5 window attend to each other:
+// S = Q K^T * scale + rel-pos bias + checkerboard mask (-100 unless query and key cell are both
+// anchors inside the image), P = softmax over keys, O = P V; output row (head*hd + d)*25 + i of the
+// unfolded map the 5x5 "fusion" conv contracts over.  Per (pixel, head) that is a 25x25xhd and a
+// 25xhdx25 product — one wave does it with v_mfma_f32_32x32x16_f16 (cells padded to 32):
+//   S^T = K . Q^T   A = K (lane = key cell j, 8 dims), B = Q^T (lane = query cell i, 8 dims);
+//                   the accumulator holds key rows j in registers and query i on the lane, so the
+//                   softmax over keys is 16 registers + one exchange with lane ^ 32;
+//   O^T = V^T . P^T P^T is used straight from the accumulator as the B operand (registers 8s..8s+7
+//                   = k-step s, key order 16s + 8(e>>2) + 4h + (e&3)); A = V^T gathered in that order.
+// Every product is split-fp16 (hi.hi + hi.lo + lo.hi, fp32 accumulation) like the conv kernels.
+// The workgroup stages the q/k/v channels of its 8x8 pixels plus a 2-cell halo in LDS once.
+#include "common.h"
+#include "kernels.h"
+
+namespace mlic {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+namespace {
+constexpr int LT = 8;             // 8x8 pixels per workgroup
+constexpr int LH = LT + 4;        // 12x12 staged cells
+constexpr int NCELL = LH * LH;
+
+__device__ __forceinline__ void split8(const float (&v)[8], half8& hi, half8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const _Float16 h = (_Float16)v[e];
+    hi[e] = h;
+    lo[e] = (_Float16)(v[e] - (float)h);
+  }
+}
+
+__device__ __forceinline__ floatx16 mfma3(const half8& ah, const half8& al, const half8& bh, const half8& bl,
+                                          floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+}
+}  // namespace
+
+template <int HD>
+__global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int C = 2 * HD;
+  const int H = P.H, W = P.W, HW = H * W;
+  const int b = blockIdx.y;
+  const int ntx = (W + LT - 1) / LT;
+  const int x0 = (blockIdx.x % ntx) * LT, y0 = (blockIdx.x / ntx) * LT;
+  const float* src = P.qkv + (int64_t)b * P.qkv_bs;
+  for (int i = threadIdx.x; i < 3 * C * NCELL; i += 256) {
+    const int ch = i / NCELL, cell = i - ch * NCELL;
+    const int gy = y0 - 2 + cell / LH, gx = x0 - 2 + cell % LH;
+    sm[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? src[(int64_t)ch * HW + gy * W + gx] : 0.0f;
+  }
+  __syncthreads();
+  const float* qs = sm;
+  const float* ks = sm + C * NCELL;
+  const float* vs = sm + 2 * C * NCELL;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const bool lvalid = l32 < 25;  // this lane's window cell (query i for S^T's B, key j for its A)
+  const int cy = lvalid ? l32 / 5 : 0, cx = lvalid ? l32 % 5 : 0;
+
+  // relative-position bias for (query i = l32, key j of register r), both heads: item-invariant
+  float bias[2][16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      bias[hh][r] = (lvalid && j < 25) ? P.rel_table[P.rel_index[l32 * 25 + j] * 2 + hh] : 0.0f;
+  }
+
+  for (int item = wave; item < 2 * LT * LT; item += 4) {
+    const int hh = item & 1, pl = item >> 1;
+    const int ly = pl / LT, lx = pl - (pl / LT) * LT;
+    const int py = y0 + ly, px = x0 + lx;
+    if (py >= H || px >= W) continue;  // wave-uniform
+    const int cell = (ly + cy) * LH + (lx + cx);
+
+    // ---- S^T = K Q^T (k = head dims, 16 per MFMA k-step)
+    floatx16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.0f;
+#pragma unroll
+    for (int k0 = 0; k0 < HD; k0 += 16) {
+      float kv[8], qv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = (k0 + 8 * h + e) * 2 + hh;  // interleaved head split: channel = d * heads + head
+        kv[e] = lvalid ? ks[ch * NCELL + cell] : 0.0f;
+        qv[e] = lvalid ? qs[ch * NCELL + cell] * P.scale : 0.0f;
+      }
+      half8 kh_, kl_, qh_, ql_;
+      split8(kv, kh_, kl_);
+      split8(qv, qh_, ql_);
+      s = mfma3(kh_, kl_, qh_, ql_, s);
+    }
+
+    // ---- bias, checkerboard mask, softmax over keys (registers + partner lane)
+    const int par = py + px;
+    const int qgy = py + cy - 2, qgx = px + cx - 2;
+    const bool qa = lvalid && qgy >= 0 && qgy < H && qgx >= 0 && qgx < W && ((par + cy + cx) & 1);
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int jy = j / 5, jx = j - 5 * (j / 5);
+      const int kgy = py + jy - 2, kgx = px + jx - 2;
+      const bool ka = kgy >= 0 && kgy < H && kgx >= 0 && kgx < W && ((par + jy + jx) & 1);
+      const float v = s[r] + bias[hh][r] + ((qa && ka) ? 0.0f : -100.0f);
+      s[r] = j < 25 ? v : -3.0e38f;
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sum = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+      s[r] = j < 25 ? expf(s[r] - mx) : 0.0f;
+      sum += s[r];
+    }
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.0f / sum;
+
+    // ---- O^T = V^T P^T (k = keys; P^T registers 8t..8t+7 are k-step t)
+    floatx16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float pv[8], vv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pv[e] = s[8 * t + e] * inv;
+        const int j = 16 * t + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int jy = j / 5, jx = j - 5 * (j / 5);
+        const int d = l32;  // A row = head dim
+        vv[e] = (j < 25 && d < HD) ? vs[((d * 2) + hh) * NCELL + (ly + jy) * LH + (lx + jx)] : 0.0f;
+      }
+      half8 ph, pl_, vh, vl;
+      split8(pv, ph, pl_);
+      split8(vv, vh, vl);
+      o = mfma3(vh, vl, ph, pl_, o);
+    }
+
+    // ---- store O^T[d][i]: T row (head * hd + d) * 25 + i at pixel p
+    if (lvalid) {
+      float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)py * W + px;
+#pragma unroll
+      for (int r = 0; r < (HD == 16 ? 8 : 16); ++r) {
+        const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+        dst[(int64_t)((hh * HD + d) * 25 + l32) * HW] = o[r];
+      }
+    }
+  }
+}
+
+void local_attn_mfma(const LocalAttnParams& P, hipStream_t st) {
+  const size_t lds = (size_t)3 * P.C * NCELL * sizeof(float);
+  MLIC_CHECK(lds <= 160 * 1024, "local attention LDS");
+  const int ntx = (P.W + LT - 1) / LT, nty = (P.H + LT - 1) / LT;
+  if (P.C == 32) hipLaunchKernelGGL(local_attn_mfma_kernel<16>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  else if (P.C == 64) hipLaunchKernelGGL(local_attn_mfma_kernel<32>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  else MLIC_CHECK(false, "LocalContext dim must be 32 or 64");
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace mlic

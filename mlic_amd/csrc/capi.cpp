@@ -328,6 +328,24 @@ int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias,
   });
 }
 
+int mlic_local_attn_run(void* stream, int impl, const float* qkv, const float* rel_table, const int32_t* rel_index,
+                        float* out, int C, int H, int W, int B, float scale) {
+  return guard([&] {
+    LocalAttnParams A{};
+    A.qkv = qkv;
+    A.qkv_bs = (int64_t)3 * C * H * W;
+    A.out = out;
+    A.out_bs = (int64_t)25 * C * H * W;
+    A.rel_table = rel_table;
+    A.rel_index = rel_index;
+    A.scale = scale;
+    A.C = C; A.H = H; A.W = W; A.B = B;
+    if (impl == 0) local_attn_valu(A, (hipStream_t)stream);
+    else local_attn_mfma(A, (hipStream_t)stream);
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  });
+}
+
 int mlic_local_attn_mask(void* stream, float* out, int H, int W) {
   return guard([&] { local_mask(out, H, W, (hipStream_t)stream); });
 }

@@ -12,7 +12,8 @@
 //    tile of loads is always in flight behind the MFMAs.  No barriers after the weight load.
 //    Per 32-pixel tile: Cout/32 x K/16 x 3 MFMAs; A reads 4*Cout*K bytes of LDS (85 B/clk/CU at
 //    K = Cout = 192, under the 128 B/clk LDS rate), so the kernel is HBM-bound:
-//    bytes/pixel = 4*(Cin + Cout [+ Cout for the GDN/residual operand]).
+//    bytes/pixel = 4*(Cin + Cout [+ Cout for the GDN/residual operand]).  Stride 2 (the 1x1 skip of
+//    ResidualBlockWithStride) only changes the per-lane input offset.
 //
 // 2. conv3x3_narrow_kernel — 3x3 stride-1 convs with Cout <= 16 (g_s's last subpel conv, N -> 12).
 //    On MFMA a 12-row output wastes >80 % of a 64-row tile; as a direct convolution on the fp32
@@ -90,8 +91,10 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
   constexpr bool square = MODE >= 2;  // GDN/IGDN convolve x*x
   const float* xbase = P.seg[0].p;
   const int64_t xbs = P.seg[0].bs;
-  const uint32_t hw4 = (uint32_t)HW * 4u;
+  const uint32_t hw4 = (uint32_t)(P.H * P.W) * 4u;  // input plane (stride 2: the full-resolution plane)
+  const uint32_t ho4 = (uint32_t)HW * 4u;           // output / aux plane
   const uint32_t img_bytes = (uint32_t)CIN * hw4;
+  const int S = P.stride;
 
   // per-tile buffer descriptor over one image's CIN planes; per-lane pixel offset in voffset,
   // the (uniform) channel offset in soffset
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
   auto voff_of = [&](int t) {
     const int b = t / tpi;
     const int p = min(((t - b * tpi) << 5) + l32, HW - 1);
-    return (uint32_t)p * 4u + (uint32_t)(8 * h) * hw4;
+    const int pin = S == 1 ? p : (p / P.Wo) * S * P.W + (p % P.Wo) * S;
+    return (uint32_t)pin * 4u + (uint32_t)(8 * h) * hw4;
   };
 
   // load ring: D = KS/2 k-steps ahead.  Slot j % D holds k-step j of the current tile until it is
@@ -184,8 +188,8 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
     const auto rs_out = make_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
     constexpr bool gdn = MODE >= 2, igdn = MODE == 3, gelu = MODE == 1;
     constexpr bool res = RES;
-    const auto rs_aux = make_rsrc(gdn ? P.aux + (int64_t)b * P.aux_bs : P.out, gdn ? (uint32_t)P.Cout * hw4 : 0u);
-    const uint32_t vo_aux = (uint32_t)p * 4u + (uint32_t)(4 * h) * hw4;
+    const auto rs_aux = make_rsrc(gdn ? P.aux + (int64_t)b * P.aux_bs : P.out, gdn ? (uint32_t)P.Cout * ho4 : 0u);
+    const uint32_t vo_aux = (uint32_t)p * 4u + (uint32_t)(4 * h) * ho4;
     const auto rs_res = make_rsrc(res ? P.res + (int64_t)b * P.res_bs : P.out, res ? (uint32_t)P.Cout * cs4 : 0u);
     const float* sb = sbias + 4 * h;  // per-lane base; the channel part folds into the ds_read offset
     // per co-tile: issue the 16 aux / residual loads together, then one wait, then 16 stores
@@ -200,7 +204,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
           if (r > 0) {
             const uint32_t step = ((r & 3) == 0) ? 5u : 1u;  // co_u = 32c + (r&3) + 8(r>>2)
             oo += step * cs4;
-            oa += step * hw4;
+            oa += step * ho4;
             opaque(oo);
             opaque(oa);
           }
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
         }
         so_o += 32 * cs4;
-        so_a += 32 * hw4;
+        so_a += 32 * ho4;
         opaque(so_o);
         opaque(so_a);
       }
@@ -243,11 +247,13 @@ static int num_cus() {
 }
 
 bool pw_resident_ok(const ConvParams& P, int cin_pad) {
-  if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1) return false;
+  if (P.K != 1 || (P.stride != 1 && P.stride != 2) || P.pad != 0 || P.nseg != 1) return false;
   if (P.epi & ~(EPI_GELU | EPI_GDN | EPI_IGDN | EPI_SQUARE_IN | EPI_RES)) return false;
   if ((P.epi & EPI_GELU) && (P.epi & (EPI_GDN | EPI_IGDN))) return false;
   if (((P.epi & (EPI_GDN | EPI_IGDN)) != 0) != ((P.epi & EPI_SQUARE_IN) != 0)) return false;
-  if (P.Ho != P.H || P.Wo != P.W || P.seg[0].C != P.Cin || cin_pad != P.Cin) return false;
+  if (P.Ho != (P.H - 1) / P.stride + 1 || P.Wo != (P.W - 1) / P.stride + 1) return false;
+  if (P.seg[0].C != P.Cin || cin_pad != P.Cin) return false;
+  if (P.stride != 1 && (P.epi & (EPI_GDN | EPI_IGDN))) return false;  // GDN aux is the conv input
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
   const int ct = (P.Cout + 31) / 32;

@@ -87,7 +87,9 @@ struct LocalAttnParams {
   float scale;
   int C, H, W, B;
 };
-void local_attn(const LocalAttnParams& P, hipStream_t st);
+void local_attn(const LocalAttnParams& P, hipStream_t st);       // MFMA (attn_local.hip) unless MLIC_LOCAL_ATTN_VALU=1
+void local_attn_mfma(const LocalAttnParams& P, hipStream_t st);
+void local_attn_valu(const LocalAttnParams& P, hipStream_t st);
 
 void softmax_spatial(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int mask_mode,
                      hipStream_t st);

@@ -15,6 +15,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace mlic {
 
 // =============================================================================================
@@ -288,6 +290,15 @@ __global__ __launch_bounds__(256) void local_attn_kernel(LocalAttnParams P) {
 }
 
 void local_attn(const LocalAttnParams& P, hipStream_t st) {
+  static const bool valu = [] {
+    const char* e = std::getenv("MLIC_LOCAL_ATTN_VALU");
+    return e && std::atoi(e) != 0;
+  }();
+  if (valu) local_attn_valu(P, st);
+  else local_attn_mfma(P, st);
+}
+
+void local_attn_valu(const LocalAttnParams& P, hipStream_t st) {
   MLIC_CHECK(P.C % 2 == 0 && P.C / 2 <= 32, "local attention head dim");
   const size_t lds = (size_t)(3 * P.C * LA_HALO * LA_HALO + 2 * 625) * sizeof(float);
   MLIC_CHECK(lds <= 160 * 1024, "local attention LDS");

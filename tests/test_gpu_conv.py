@@ -70,6 +70,11 @@ def test_pw_resident_epilogues(epi):
     check(*run(PW, 2, 192, 192, 36, 60, 1, epi=epi))
 
 
+def test_pw_resident_stride2():
+    check(*run(PW, 2, 192, 192, 68, 96, 1, stride=2))
+    check(*run(PW, 1, 128, 128, 37, 51, 1, stride=2, epi=GELU))  # odd sizes: ragged tiles
+
+
 def test_pw_resident_ragged_and_many_tiles():
     check(*run(PW, 3, 192, 192, 37, 53, 1))   # 1961 px: tail tile per image
     check(*run(PW, 2, 192, 192, 136, 240, 1))  # > 2048 tiles: every wave loops
@@ -144,3 +149,37 @@ def test_depthwise(shape):
     if gelu:
         ref = F.gelu(ref)
     check(y, ref.float(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("ch,H,W,B", [(32, 24, 40, 2), (64, 13, 21, 1), (32, 68, 120, 1)])
+def test_local_attention_kernels(ch, H, W, B):
+    """Both LocalContext attention kernels vs a float64 torch restatement of context.py:75-107."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import mlic_ref_cpu as ref
+    from mlic_amd import _lib, synthetic
+    g = torch.Generator().manual_seed(3)
+    dev = torch.device("cuda")
+    heads, hd, L = 2, ch // 2, H * W
+    qkv = (torch.randn(B, 3 * ch, H, W, generator=g) * 2).to(dev)
+    table = torch.randn(81, 2, generator=g).to(dev)
+    index = torch.from_numpy(synthetic.relative_position_index(5)).reshape(-1).to(torch.int32).to(dev)
+    scale = hd ** -0.5
+    x = qkv.double()
+    wins = F.unfold(x, kernel_size=5, padding=2).permute(0, 2, 1).reshape(B, L, 3, ch, 25).permute(2, 0, 1, 3, 4)
+
+    def heads_split(t):  # channel c = d * heads + h
+        return t.reshape(B, L, hd, heads, 25).permute(0, 1, 3, 4, 2)
+    q, k, v = heads_split(wins[0]) * scale, heads_split(wins[1]), heads_split(wins[2])
+    bias = table.double()[index.long()].view(25, 25, 2).permute(2, 0, 1)
+    mask = ref.local_attn_mask(H, W, 5).double().to(dev)
+    attn = torch.softmax(q @ k.transpose(-2, -1) + bias[None, None] + mask[None, :, None], dim=-1)
+    expect = (attn @ v).permute(0, 2, 4, 3, 1).reshape(B, ch * 25, H, W).float()  # row (h * hd + d) * 25 + i
+    st = torch.cuda.current_stream().cuda_stream
+    for impl in (0, 1):
+        out = torch.full((B, 25 * ch, H, W), float("nan"), device=dev)
+        _lib.call("mlic_local_attn_run", C.c_void_p(st), impl, C.c_void_p(qkv.data_ptr()),
+                  C.c_void_p(table.data_ptr()), C.c_void_p(index.data_ptr()), C.c_void_p(out.data_ptr()),
+                  ch, H, W, B, float(scale))
+        check(out, expect, rtol=2e-5)
