@@ -11,7 +11,10 @@
 //   O^T = V^T . P^T P^T is used straight from the accumulator as the B operand (registers 8s..8s+7
 //                   = k-step s, key order 16s + 8(e>>2) + 4h + (e&3)); A = V^T gathered in that order.
 // Every product is split-fp16 (hi.hi + hi.lo + lo.hi, fp32 accumulation) like the conv kernels.
-// The workgroup stages the q/k/v channels of its 8x8 pixels plus a 2-cell halo in LDS once.
+// The workgroup stages the q/k/v channels of its pixel tile plus a 2-cell halo in LDS once.  For
+// hd = 16 the tile is a 1 x 32 strip and each head's 400 x 32 output block is staged in LDS and
+// written as 128-byte rows (the per-lane results are 25 different rows of one pixel — written
+// directly they are 4-byte scattered stores); hd = 32 (MLICPP_S2) uses 8 x 8 tiles, direct stores.
 #include "common.h"
 #include "kernels.h"
 
@@ -21,9 +24,14 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 namespace {
-constexpr int LT = 8;             // 8x8 pixels per workgroup
-constexpr int LH = LT + 4;        // 12x12 staged cells
-constexpr int NCELL = LH * LH;
+template <int HD>
+struct LaTile {
+  static constexpr bool STAGE = HD == 16;
+  static constexpr int TH = STAGE ? 1 : 8, TW = STAGE ? 32 : 8;
+  static constexpr int LH = TH + 4, LW = TW + 4, NCELL = LH * LW, NPIX = TH * TW;
+  static constexpr int OPITCH = NPIX + 1;  // staged output row pitch (conflict-free lane writes)
+  static constexpr size_t lds_floats(int C) { return (size_t)3 * C * NCELL + (STAGE ? HD * 25 * OPITCH : 0); }
+};
 
 __device__ __forceinline__ void split8(const float (&v)[8], half8& hi, half8& lo) {
 #pragma unroll
@@ -45,17 +53,19 @@ __device__ __forceinline__ floatx16 mfma3(const half8& ah, const half8& al, cons
 template <int HD>
 __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  constexpr int C = 2 * HD;
+  using T = LaTile<HD>;
+  constexpr int C = 2 * HD, LT_H = T::TH, LT_W = T::TW, LW = T::LW, NCELL = T::NCELL;
   const int H = P.H, W = P.W, HW = H * W;
   const int b = blockIdx.y;
-  const int ntx = (W + LT - 1) / LT;
-  const int x0 = (blockIdx.x % ntx) * LT, y0 = (blockIdx.x / ntx) * LT;
+  const int ntx = (W + LT_W - 1) / LT_W;
+  const int x0 = (blockIdx.x % ntx) * LT_W, y0 = (blockIdx.x / ntx) * LT_H;
   const float* src = P.qkv + (int64_t)b * P.qkv_bs;
   for (int i = threadIdx.x; i < 3 * C * NCELL; i += 256) {
     const int ch = i / NCELL, cell = i - ch * NCELL;
-    const int gy = y0 - 2 + cell / LH, gx = x0 - 2 + cell % LH;
+    const int gy = y0 - 2 + cell / LW, gx = x0 - 2 + cell % LW;
     sm[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? src[(int64_t)ch * HW + gy * W + gx] : 0.0f;
   }
+  float* ostage = sm + 3 * C * NCELL;  // [HD * 25][OPITCH] (STAGE only)
   __syncthreads();
   const float* qs = sm;
   const float* ks = sm + C * NCELL;
@@ -76,12 +86,13 @@ __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P)
       bias[hh][r] = (lvalid && j < 25) ? P.rel_table[P.rel_index[l32 * 25 + j] * 2 + hh] : 0.0f;
   }
 
-  for (int item = wave; item < 2 * LT * LT; item += 4) {
-    const int hh = item & 1, pl = item >> 1;
-    const int ly = pl / LT, lx = pl - (pl / LT) * LT;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+  for (int pl = wave; pl < T::NPIX; pl += 4) {
+    const int ly = pl / LT_W, lx = pl - (pl / LT_W) * LT_W;
     const int py = y0 + ly, px = x0 + lx;
     if (py >= H || px >= W) continue;  // wave-uniform
-    const int cell = (ly + cy) * LH + (lx + cx);
+    const int cell = (ly + cy) * LW + (lx + cx);
 
     // ---- S^T = K Q^T (k = head dims, 16 per MFMA k-step)
     floatx16 s;
@@ -141,7 +152,7 @@ __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P)
         const int j = 16 * t + 8 * (e >> 2) + 4 * h + (e & 3);
         const int jy = j / 5, jx = j - 5 * (j / 5);
         const int d = l32;  // A row = head dim
-        vv[e] = (j < 25 && d < HD) ? vs[((d * 2) + hh) * NCELL + (ly + jy) * LH + (lx + jx)] : 0.0f;
+        vv[e] = (j < 25 && d < HD) ? vs[((d * 2) + hh) * NCELL + (ly + jy) * LW + (lx + jx)] : 0.0f;
       }
       half8 ph, pl_, vh, vl;
       split8(pv, ph, pl_);
@@ -149,26 +160,51 @@ __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P)
       o = mfma3(vh, vl, ph, pl_, o);
     }
 
-    // ---- store O^T[d][i]: T row (head * hd + d) * 25 + i at pixel p
+    // ---- O^T[d][i] -> T row (head * hd + d) * 25 + i at pixel p
     if (lvalid) {
-      float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)py * W + px;
+      if constexpr (T::STAGE) {
 #pragma unroll
-      for (int r = 0; r < (HD == 16 ? 8 : 16); ++r) {
-        const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
-        dst[(int64_t)((hh * HD + d) * 25 + l32) * HW] = o[r];
+        for (int r = 0; r < 8; ++r) {
+          const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+          ostage[(d * 25 + l32) * T::OPITCH + pl] = o[r];
+        }
+      } else {
+        float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)py * W + px;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+          dst[(int64_t)((hh * HD + d) * 25 + l32) * HW] = o[r];
+        }
       }
     }
   }
+  if constexpr (T::STAGE) {  // coalesced write of this head's rows (one 32-pixel strip each)
+    __syncthreads();
+    const int nvalid = min(LT_W, W - x0);
+    float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)(hh * HD * 25) * HW + (int64_t)y0 * W + x0;
+    for (int idx = threadIdx.x; idx < HD * 25 * T::NPIX; idx += 256) {
+      const int row = idx / T::NPIX, pix = idx - row * T::NPIX;
+      if (pix < nvalid) dst[(int64_t)row * HW + pix] = ostage[row * T::OPITCH + pix];
+    }
+    __syncthreads();
+  }
+  }
+}
+
+template <int HD>
+static void launch_la(const LocalAttnParams& P, hipStream_t st) {
+  using T = LaTile<HD>;
+  const size_t lds = T::lds_floats(P.C) * sizeof(float);
+  MLIC_CHECK(lds <= 160 * 1024, "local attention LDS");
+  const int ntx = (P.W + T::TW - 1) / T::TW, nty = (P.H + T::TH - 1) / T::TH;
+  hipLaunchKernelGGL(local_attn_mfma_kernel<HD>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  HIP_OK(hipGetLastError());
 }
 
 void local_attn_mfma(const LocalAttnParams& P, hipStream_t st) {
-  const size_t lds = (size_t)3 * P.C * NCELL * sizeof(float);
-  MLIC_CHECK(lds <= 160 * 1024, "local attention LDS");
-  const int ntx = (P.W + LT - 1) / LT, nty = (P.H + LT - 1) / LT;
-  if (P.C == 32) hipLaunchKernelGGL(local_attn_mfma_kernel<16>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
-  else if (P.C == 64) hipLaunchKernelGGL(local_attn_mfma_kernel<32>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  if (P.C == 32) launch_la<16>(P, st);
+  else if (P.C == 64) launch_la<32>(P, st);
   else MLIC_CHECK(false, "LocalContext dim must be 32 or 64");
-  HIP_OK(hipGetLastError());
 }
 
 }  // namespace mlic

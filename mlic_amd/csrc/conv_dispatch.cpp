@@ -11,7 +11,10 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (precision == 1) return CONV_X3;
   // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
   if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
-  if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && conv_halo_ok(P, w.cin_pad)) return CONV_HALO;
+  // halo 3x3: enough 128 x 256 tiles to fill the chip
+  if (conv_halo_ok(P, w.cin_pad) &&
+      (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 7) / 8) * P.B >= 256)
+    return CONV_HALO;
   return CONV_X3V2;
 }
 

@@ -151,6 +151,57 @@ __global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
   }
 }
 
+// stride-2 fast path: 16x64 output tile from a (33 x 136)-float patch (patch column 0 = input
+// column 2*ox0 - 4, aligned float4 loads); each thread makes 4 horizontally adjacent outputs from
+// 3 rows x 9 inputs (two float4 + one scalar LDS read per row).
+constexpr int DW2_TH = 16, DW2_TW = 64, DW2_PR = 2 * DW2_TH + 1, DW2_PQ = 2 * DW2_TW / 4 + 2;
+__global__ __launch_bounds__(256) void dw3x3_s2_vec_kernel(DwParams P) {
+  __shared__ float4 tile[DW2_PR * DW2_PQ];
+  const int c = blockIdx.y, b = blockIdx.z;
+  const int ntx = (P.Wo + DW2_TW - 1) / DW2_TW;
+  const int ox0 = (blockIdx.x % ntx) * DW2_TW, oy0 = (blockIdx.x / ntx) * DW2_TH;
+  int sg = 0, c0 = 0;
+  while (sg + 1 < P.nseg && c >= c0 + P.seg[sg].C) { c0 += P.seg[sg].C; ++sg; }
+  const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
+  const int W4 = P.W >> 2;
+  const float4* src4 = reinterpret_cast<const float4*>(src);
+  for (int i = threadIdx.x; i < DW2_PR * DW2_PQ; i += 256) {
+    const int r = i / DW2_PQ, q = i - r * DW2_PQ;
+    const int gy = 2 * oy0 - 1 + r, gq = (2 * ox0 >> 2) - 1 + q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gy >= 0 && gy < P.H && gq >= 0 && gq < W4) v = src4[(int64_t)gy * W4 + gq];
+    tile[i] = v;
+  }
+  __syncthreads();
+  float w[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w[k] = P.w[c * 9 + k];
+  const float bias = P.bias ? P.bias[c] : 0.0f;
+  const int cg = threadIdx.x & 15, ry = threadIdx.x >> 4;  // outputs (oy0 + ry, ox0 + 4cg .. +3)
+  const float* tf = reinterpret_cast<const float*>(tile);
+  constexpr int PITCH = DW2_PQ * 4;
+  float o[4] = {bias, bias, bias, bias};
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    // input cols 8cg-1 .. 8cg+7  <->  patch cols 8cg+3 .. 8cg+11
+    const int pr = 2 * ry + ky;
+    const float4 m0 = tile[pr * DW2_PQ + 2 * cg + 1], m1 = tile[pr * DW2_PQ + 2 * cg + 2];
+    const float in[9] = {tf[pr * PITCH + 8 * cg + 3], m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) o[q] = fmaf(w[ky * 3 + kx], in[2 * q + kx], o[q]);
+  }
+  if (P.gelu) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = gelu_erf(o[q]);
+  }
+  const int oy = oy0 + ry, ox = ox0 + 4 * cg;
+  if (oy < P.Ho && ox < P.Wo)
+    *reinterpret_cast<float4*>(P.out + (int64_t)b * P.out_bs + (int64_t)c * P.Ho * P.Wo + (int64_t)oy * P.Wo + ox) =
+        make_float4(o[0], o[1], o[2], o[3]);
+}
+
 void dw3x3(const DwParams& P, hipStream_t st) {
   MLIC_CHECK(P.stride == 1 || P.stride == 2, "dw stride");
   MLIC_CHECK(P.Ho == (P.H - 1) / P.stride + 1 && P.Wo == (P.W - 1) / P.stride + 1, "dw output size");
@@ -164,6 +215,12 @@ void dw3x3(const DwParams& P, hipStream_t st) {
   if (P.stride == 1 && aligned) {
     const int ntx = (P.Wo + DWF_TW - 1) / DWF_TW, nty = (P.Ho + DWF_TH - 1) / DWF_TH;
     hipLaunchKernelGGL(dw3x3_s1_vec_kernel, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  if (P.stride == 2 && aligned && (P.Wo % 4) == 0) {
+    const int ntx = (P.Wo + DW2_TW - 1) / DW2_TW, nty = (P.Ho + DW2_TH - 1) / DW2_TH;
+    hipLaunchKernelGGL(dw3x3_s2_vec_kernel, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
     HIP_OK(hipGetLastError());
     return;
   }

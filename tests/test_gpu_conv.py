@@ -111,7 +111,7 @@ def test_generic_tiles(impl, shape):
     (1, 192, 768, 19, 45, SHUFFLE),          # ragged tiles at every edge
     (2, 96, 192, 16, 32, GELU | RES),        # Cout not a multiple of 128, residual
     (1, 160, 96, 9, 40, 0),                  # Cin 160 (5 chunks), Cout < 128
-    (1, 100, 64, 8, 32, GDN | SQUARE),       # Cin not a multiple of 32 (zero-padded chunk)
+    (1, 100, 100, 8, 32, GDN | SQUARE),      # Cin not a multiple of 32 (zero-padded chunk)
 ])
 def test_halo(shape):
     B, cin, cout, H, W, epi = shape
@@ -129,7 +129,8 @@ def test_auto_matches_selected_family():
     (2, 192, 64, 256, 1, 0),   # vectorised stride-1 path, 2 x 2 tiles
     (2, 192, 40, 100, 1, 1),   # W % 4 == 0, ragged tiles, GELU
     (1, 96, 37, 53, 1, 0),     # W % 4 != 0: generic path
-    (2, 192, 64, 96, 2, 0),    # stride 2
+    (2, 192, 64, 96, 2, 0),    # stride 2, vectorised path (W % 8 == 0)
+    (2, 192, 68, 120, 2, 1),   # stride 2, ragged tile, GELU
     (1, 3, 65, 97, 2, 0),      # 3-channel stride-2 input conv, odd sizes
 ])
 def test_depthwise(shape):
