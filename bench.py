@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 # the split-fp16 kernels issue 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of
 # fp32-equivalent work; the VALU conv kernels run exact fp32 FMAs (157.3 TF with packed FMA)
 def kernel_peak(name: str):
-    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv3x3_halo")):
+    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv_halo")):
         return 2500.0 / 3, "3 x v_mfma_f32_32x32x16_f16 per fp32 product (split-fp16)"
     if name.startswith("conv_mfma"):
         return 157.3, "v_mfma_f32_32x32x2_f32"
@@ -185,27 +185,51 @@ def main():
     h = net._handle
     _lib.call("mlic_set_lanes", h, 1)  # events on overlapping lanes would double-count device time
     _lib.call("mlic_set_profiling", h, 1)
-    step()
-    torch.cuda.synchronize()
-    _lib.call("mlic_set_profiling", h, 0)
-    net.set_lanes(a.lanes)
-    if a.layers_out:
-        n = C.c_size_t()
-        _lib.call("mlic_profile_layers", h, None, 0, C.byref(n))
-        buf = C.create_string_buffer(n.value + 1)
-        _lib.call("mlic_profile_layers", h, buf, n.value + 1, C.byref(n))
-        if rank == 0:
-            with open(a.layers_out, "w") as f:
-                f.write(buf.value.decode())
-    fam = {}
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
+    names = []
     for cat in range(ncat.value):
         nb = C.create_string_buffer(128)
         _lib.call("mlic_profile_category_name", cat, nb, 128)
-        n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
-        _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
-        fam[nb.value.decode()] = {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
+        names.append(nb.value.decode())
+    fam = {nm: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0} for nm in names}
+    layer_rows = []
+    phase_gpu = {}
+
+    def harvest(tag):
+        # per-layer table (before the reads, which clear), then per-family sums
+        if a.layers_out:
+            n = C.c_size_t()
+            _lib.call("mlic_profile_layers", h, None, 0, C.byref(n))
+            buf = C.create_string_buffer(n.value + 1)
+            _lib.call("mlic_profile_layers", h, buf, n.value + 1, C.byref(n))
+            lines = buf.value.decode().splitlines()
+            if not layer_rows:
+                layer_rows.append("phase\t" + lines[0])
+            layer_rows.extend(f"{tag}\t{ln}" for ln in lines[1:])
+        tot = 0.0
+        for cat, nm in enumerate(names):
+            n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
+            _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
+            f = fam[nm]
+            f["launches"] += n.value
+            f["ms"] += ms.value
+            f["flops"] += fl.value
+            f["bytes"] += by.value
+            tot += ms.value
+        phase_gpu[tag] = round(tot, 3)
+
+    c = net.compress(x)
+    torch.cuda.synchronize()
+    harvest("compress")
+    net.decompress(c["strings"], c["shape"])
+    torch.cuda.synchronize()
+    harvest("decompress")
+    _lib.call("mlic_set_profiling", h, 0)
+    net.set_lanes(a.lanes)
+    if a.layers_out and rank == 0:
+        with open(a.layers_out, "w") as f:
+            f.write("\n".join(layer_rows) + "\n")
     # dominant kernel = the conv kernel instantiation with the most device time; its roofline bound
     # is whichever ceiling is lower at its arithmetic intensity (algorithmic FLOPs / bytes)
     convs = [k for k in fam if is_conv(k)]
@@ -260,6 +284,7 @@ def main():
                          "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3)},
             "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
+            "gpu_kernel_ms_by_phase": phase_gpu,
             "host_thread_ms_per_step": host,
             "wall_ms_per_step": wall_split,
             "lanes": a.lanes,

@@ -24,6 +24,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 namespace {
+// 8 waves: the 120 KB of LDS admits one workgroup per CU, so the block itself must bring 2 waves per SIMD
+constexpr int LA_THREADS = 512;
+constexpr int LA_WAVES = LA_THREADS / 64;
+
 template <int HD>
 struct LaTile {
   static constexpr bool STAGE = HD == 16;
@@ -51,7 +55,7 @@ __device__ __forceinline__ floatx16 mfma3(const half8& ah, const half8& al, cons
 }  // namespace
 
 template <int HD>
-__global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P) {
+__global__ __launch_bounds__(LA_THREADS) void local_attn_mfma_kernel(LocalAttnParams P) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   using T = LaTile<HD>;
   constexpr int C = 2 * HD, LT_H = T::TH, LT_W = T::TW, LW = T::LW, NCELL = T::NCELL;
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P)
   const int ntx = (W + LT_W - 1) / LT_W;
   const int x0 = (blockIdx.x % ntx) * LT_W, y0 = (blockIdx.x / ntx) * LT_H;
   const float* src = P.qkv + (int64_t)b * P.qkv_bs;
-  for (int i = threadIdx.x; i < 3 * C * NCELL; i += 256) {
+  for (int i = threadIdx.x; i < 3 * C * NCELL; i += LA_THREADS) {
     const int ch = i / NCELL, cell = i - ch * NCELL;
     const int gy = y0 - 2 + cell / LW, gx = x0 - 2 + cell % LW;
     sm[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? src[(int64_t)ch * HW + gy * W + gx] : 0.0f;
@@ -88,7 +92,7 @@ __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P)
 
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
-  for (int pl = wave; pl < T::NPIX; pl += 4) {
+  for (int pl = wave; pl < T::NPIX; pl += LA_WAVES) {
     const int ly = pl / LT_W, lx = pl - (pl / LT_W) * LT_W;
     const int py = y0 + ly, px = x0 + lx;
     if (py >= H || px >= W) continue;  // wave-uniform
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256) void local_attn_mfma_kernel(LocalAttnParams P)
     __syncthreads();
     const int nvalid = min(LT_W, W - x0);
     float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)(hh * HD * 25) * HW + (int64_t)y0 * W + x0;
-    for (int idx = threadIdx.x; idx < HD * 25 * T::NPIX; idx += 256) {
+    for (int idx = threadIdx.x; idx < HD * 25 * T::NPIX; idx += LA_THREADS) {
       const int row = idx / T::NPIX, pix = idx - row * T::NPIX;
       if (pix < nvalid) dst[(int64_t)row * HW + pix] = ostage[row * T::OPITCH + pix];
     }
@@ -197,7 +201,7 @@ static void launch_la(const LocalAttnParams& P, hipStream_t st) {
   const size_t lds = T::lds_floats(P.C) * sizeof(float);
   MLIC_CHECK(lds <= 160 * 1024, "local attention LDS");
   const int ntx = (P.W + T::TW - 1) / T::TW, nty = (P.H + T::TH - 1) / T::TH;
-  hipLaunchKernelGGL(local_attn_mfma_kernel<HD>, dim3(ntx * nty, P.B), dim3(256), lds, st, P);
+  hipLaunchKernelGGL(local_attn_mfma_kernel<HD>, dim3(ntx * nty, P.B), dim3(LA_THREADS), lds, st, P);
   HIP_OK(hipGetLastError());
 }
 

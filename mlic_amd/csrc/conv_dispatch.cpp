@@ -12,7 +12,7 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
   if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
   // halo 3x3: enough 128 x 256 tiles to fill the chip
-  if (conv_halo_ok(P, w.cin_pad) &&
+  if (P.K == 3 && conv_halo_ok(P, w.cin_pad) &&
       (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 7) / 8) * P.B >= 256)
     return CONV_HALO;
   return CONV_X3V2;
@@ -49,7 +49,7 @@ const char* prof_cat_name(int cat) {
       "conv_mfma_kernel<128,128>",   "conv_f16x3_kernel<32,256>", "conv_f16x3_kernel<64,128>",
       "conv_f16x3_kernel<128,64>",   "conv_f16x3_kernel<128,128>", "conv_x3v2_kernel<64,128>",
       "conv_x3v2_kernel<128,256>",   "conv_x3v2_kernel<128,128>", "pw_resident_kernel",
-      "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "conv3x3_halo_kernel",
+      "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "conv_halo_kernel",
       "dw3x3_kernel",
       "local_attn_kernel",           "linear_attention",          "elementwise"};
   return (cat >= 0 && cat < PCAT_COUNT) ? names[cat] : "";

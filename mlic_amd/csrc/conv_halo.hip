@@ -1,20 +1,22 @@
-// Halo-tiled 3x3 stride-1 convolution on the split-fp16 MFMA pipe (gfx950).
+// Halo-tiled KxK stride-1 convolution / 1x1 GEMM on the split-fp16 MFMA pipe (gfx950).
 //
 // The dense 3x3 convs of g_s / h_s (subpel N -> 4N with PixelShuffle, mlicpp synthesis) are the
 // largest GEMMs of the step.  As an implicit GEMM with a BK=32 K-step per tap (conv_x3v2) every
 // K-step re-reads both operands from L2 — 32 KB per 128x128x32 block step, ~25 TB/s of L2 traffic
 // at full MFMA rate, which is where that kernel saturates.  Here a block owns a 128(Cout) x
-// 8x32(pixels) output tile and walks the input in 32-channel chunks:
-//   * the chunk's (8+2) x (32+2) input patch is staged ONCE in LDS, split into hi/lo fp16 and
-//     stored channel-contiguous ([position][channel], 80-byte pitch), so each of the 9 taps reads
-//     its B fragments (8 consecutive channels of one shifted position per lane) with ds_read_b128
-//     straight from the shared patch;
+// TH x 32(pixels) output tile and walks the input in 32-channel chunks:
+//   * the chunk's (TH+K-1) x (32+K-1) input patch is staged ONCE in LDS, split into hi/lo fp16 and
+//     stored channel-contiguous ([position][channel], 80-byte pitch), so each of the K*K taps
+//     reads its B fragments (8 consecutive channels of one shifted position per lane) with
+//     ds_read_b128 straight from the shared patch;
 //   * the weights are staged per (chunk, tap) as a 128 x 32 hi/lo tile (double-buffered);
-//   * the next chunk's patch is loaded during the current chunk's first taps.
-// Per 128x256x32 step: 16 KB of weights + 1/9 of a 54 KB patch from L2 (≈ 3x less than x3v2 per
-// FLOP).  8 waves, each a 64(Cout) x 64(pixels) sub-tile: 2 x 2 v_mfma_f32_32x32x16_f16 tiles x
-// 3 split terms per 16-deep k-step.  Epilogue = the shared conv_store (bias, GELU, GDN, masks,
-// PixelShuffle, residual).
+//   * the next chunk's patch is loaded while the current chunk's first taps run.
+// K = 3, TH = 8 (g_s / h_s 3x3): per 128x256x32 step 16 KB of weights + 1/9 of a 54 KB patch from
+// L2 (~3x less than x3v2 per FLOP).  K = 1, TH = 8: the latent-resolution 1x1 GEMMs (entropy
+// parameters, LRP, context MLPs) with the same 8-wave 128x256 tile.  K = 5, TH = 4: the inter-slice
+// context reprojection.  8 waves, each a 64(Cout) x (TH/4 rows x 32) sub-tile of
+// v_mfma_f32_32x32x16_f16 x 3 split terms.  Multi-segment (channel-concat) inputs are read in
+// place (segments are 16-channel aligned).  Epilogue = the shared conv_store.
 #include "common.h"
 #include "kernels.h"
 
@@ -24,32 +26,41 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 namespace {
-constexpr int HT = 512;                    // threads (8 waves)
-constexpr int HBM = 128;                   // Cout per block
-constexpr int TH = 8, TW = 32;             // output tile (rows x cols) = 256 pixels
-constexpr int PH = TH + 2, PW = TW + 2;    // input patch
-constexpr int NPOS = PH * PW;              // 340 positions
-constexpr int CK = 32;                     // channels per chunk
-constexpr int PITCH = 40;                  // halves per LDS row (32 + 8): conflict-free b128 reads
-constexpr int A_SZ = HBM * PITCH;          // one hi or lo weight tile
-constexpr int B_SZ = NPOS * PITCH;         // one hi or lo patch
-constexpr int A_BUF = 2 * A_SZ, B_BUF = 2 * B_SZ;
-constexpr int LDS_HALVES = 2 * A_BUF + 2 * B_BUF;
-constexpr int PITEMS = NPOS * (CK / 8);    // patch staging items: 8 channels at one position
-constexpr int PSTEPS = (PITEMS + HT - 1) / HT;  // taps of a chunk that carry patch loads (3)
-static_assert(PSTEPS <= 9, "patch staging must fit in one chunk's taps");
-static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
+constexpr int HT = 512;       // threads (8 waves: 2 along Cout x 4 along pixel rows)
+constexpr int HBM = 128;      // Cout per block
+constexpr int TW = 32;        // output tile width
+constexpr int CK = 32;        // channels per chunk
+constexpr int PITCH = 40;     // halves per LDS row (32 + 8): conflict-free b128 reads
+constexpr int A_SZ = HBM * PITCH;
+constexpr int A_BUF = 2 * A_SZ;
+
+template <int K, int TH>
+struct Halo {
+  static constexpr int KK = K * K;
+  static constexpr int PH = TH + K - 1, PW = TW + K - 1, NPOS = PH * PW;
+  static constexpr int B_SZ = NPOS * PITCH, B_BUF = 2 * B_SZ;
+  static constexpr int LDS_HALVES = 2 * A_BUF + 2 * B_BUF;
+  static constexpr int PITEMS = NPOS * (CK / 8);            // staging items: 8 channels at one position
+  static constexpr int PARTS = (PITEMS + HT - 1) / HT;       // items per thread per chunk
+  static constexpr int PPT = (PARTS + KK - 1) / KK;          // parts loaded per tap
+  static constexpr int TN = TH / 4;                          // pixel rows per wave
+  static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
+  static_assert(TH % 4 == 0, "tile");
+};
 }  // namespace
 
-__global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _Float16* __restrict__ wh,
-                                                          const _Float16* __restrict__ wl, int cin_pad) {
-  __shared__ __attribute__((aligned(16))) _Float16 sm[LDS_HALVES];
+template <int K, int TH>
+__global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Float16* __restrict__ wh,
+                                                       const _Float16* __restrict__ wl, int cin_pad) {
+  using G = Halo<K, TH>;
+  constexpr int KK = G::KK, PW = G::PW, NPOS = G::NPOS, B_SZ = G::B_SZ, B_BUF = G::B_BUF, TN = G::TN;
+  __shared__ __attribute__((aligned(16))) _Float16 sm[G::LDS_HALVES];
   _Float16* As = sm;                  // [2][hi|lo][HBM][PITCH]
   _Float16* Bs = sm + 2 * A_BUF;      // [2][hi|lo][NPOS][PITCH]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves: 64 Cout x (2 rows x 32 cols)
+  const int wm = wave >> 2, wn = wave & 3;
 
   // block -> (Cout tile, spatial tile), XCD-aware bijective remap as conv_x3v2
   const int ntx = (P.Wo + TW - 1) / TW, nty = (P.Ho + TH - 1) / TH;
@@ -64,20 +75,20 @@ __global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _F
   const int co0 = ct * HBM;
   const int oy0 = (pt / ntx) * TH, ox0 = (pt % ntx) * TW;
   const int b = blockIdx.z;
-  const int H = P.H, W = P.W;
+  const int H = P.H, W = P.W, pad = P.pad;
   const int64_t HW = (int64_t)H * W;
-  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs;
   const int nchunk = cin_pad / CK;
-  const int nsteps = nchunk * 9;
+  const int nsteps = nchunk * KK;
+  const bool square = (P.epi & EPI_SQUARE_IN) != 0;
 
   // ---- staging helpers
-  uint4 ra_h, ra_l;  // one 16-byte chunk of the hi and lo weight tile per thread (128 x 32 / 512 / 8 = 1)
+  uint4 ra_h, ra_l;  // one 16-byte chunk of the hi and lo weight tile per thread
   auto load_a = [&](int s) {
-    const int c = s / 9, tap = s - 9 * (s / 9);
+    const int c = s / KK, tap = s - KK * (s / KK);
     const int row = tid >> 2, q = tid & 3;
     const int co = co0 + row;
     if (co < P.Cout) {
-      const int64_t off = ((int64_t)co * 9 + tap) * cin_pad + c * CK + 8 * q;
+      const int64_t off = ((int64_t)co * KK + tap) * cin_pad + c * CK + 8 * q;
       ra_h = *reinterpret_cast<const uint4*>(wh + off);
       ra_l = *reinterpret_cast<const uint4*>(wl + off);
     } else {
@@ -91,52 +102,54 @@ __global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _F
     *reinterpret_cast<uint4*>(base + row * PITCH + 8 * q) = ra_h;
     *reinterpret_cast<uint4*>(base + A_SZ + row * PITCH + 8 * q) = ra_l;
   };
-  float rp[8];  // 8 channels of one patch position
-  auto load_p = [&](int c, int part) {
+  float rp[G::PPT][8];  // 8 channels of one patch position, per part
+  auto load_p = [&](int c, int part, float (&dst)[8]) {
     const int item = part * HT + tid;
-    if (item >= PITEMS) return;
+    if (item >= G::PITEMS) return;
     const int pos = item % NPOS, g = item / NPOS;  // position fastest: coalesced along patch rows
     const int py = pos / PW, px = pos - py * PW;
-    const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+    const int iy = oy0 - pad + py, ix = ox0 - pad + px;
     const bool inb = iy >= 0 && iy < H && ix >= 0 && ix < W;
     const int ch0 = c * CK + 8 * g;
-    const float* src = x + (int64_t)ch0 * HW + (int64_t)iy * W + ix;
+    int s = 0, c0 = 0;  // 8-channel groups never straddle a segment (16-aligned segments)
+    while (s + 1 < P.nseg && ch0 >= c0 + P.seg[s].C) { c0 += P.seg[s].C; ++s; }
+    const Seg sg = P.seg[s];
+    const float* src = sg.p + (int64_t)b * sg.bs + (int64_t)(ch0 - c0) * HW + (int64_t)iy * W + ix;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const bool ok = inb && (ch0 + j) < P.Cin;
+      const bool ok = inb && (ch0 + j) < P.Cin && (ch0 - c0 + j) < sg.C;
       float v = ok ? src[(int64_t)j * HW] : 0.0f;
-      if (P.epi & EPI_SQUARE_IN) v *= v;
-      rp[j] = v;
+      dst[j] = square ? v * v : v;
     }
   };
-  auto store_p = [&](int buf, int part) {
+  auto store_p = [&](int buf, int part, const float (&v8)[8]) {
     const int item = part * HT + tid;
-    if (item >= PITEMS) return;
+    if (item >= G::PITEMS) return;
     const int pos = item % NPOS, g = item / NPOS;
     half8 h, l;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const _Float16 hv = (_Float16)rp[j];
+      const _Float16 hv = (_Float16)v8[j];
       h[j] = hv;
-      l[j] = (_Float16)(rp[j] - (float)hv);
+      l[j] = (_Float16)(v8[j] - (float)hv);
     }
     _Float16* base = Bs + buf * B_BUF + pos * PITCH + 8 * g;
     *reinterpret_cast<half8*>(base) = h;
     *reinterpret_cast<half8*>(base + B_SZ) = l;
   };
 
-  floatx16 acc[2][2];
+  floatx16 acc[2][TN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   // ---- prologue: chunk 0's patch and step 0's weights
-  for (int part = 0; part < PSTEPS; ++part) {
-    load_p(0, part);
-    store_p(0, part);
+  for (int part = 0; part < G::PARTS; ++part) {
+    load_p(0, part, rp[0]);
+    store_p(0, part, rp[0]);
   }
   load_a(0);
   store_a(0);
@@ -144,18 +157,22 @@ __global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _F
 
   const int l32 = lane & 31, kh = (lane >> 5) * 8;
   for (int s = 0; s < nsteps; ++s) {
-    const int c = s / 9, tap = s - 9 * c;
-    const int ky = tap / 3, kx = tap - 3 * ky;
+    const int c = s / KK, tap = s - KK * c;
+    const int ky = tap / K, kx = tap - K * ky;
     const bool more = s + 1 < nsteps;
-    const bool pstage = (c + 1 < nchunk) && tap < PSTEPS;
+    const bool pstage = (c + 1 < nchunk) && tap * G::PPT < G::PARTS;
     if (more) load_a(s + 1);
-    if (pstage) load_p(c + 1, tap);
+    if (pstage) {
+#pragma unroll
+      for (int u = 0; u < G::PPT; ++u)
+        if (tap * G::PPT + u < G::PARTS) load_p(c + 1, tap * G::PPT + u, rp[u]);
+    }
 
     const _Float16* A = As + (s & 1) * A_BUF;
     const _Float16* Bp = Bs + (c & 1) * B_BUF;
 #pragma unroll
     for (int ks = 0; ks < CK; ks += 16) {
-      half8 ah[2], al[2], bh[2], bl[2];
+      half8 ah[2], al[2], bh[TN], bl[TN];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = wm * 64 + i * 32 + l32;
@@ -163,15 +180,15 @@ __global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _F
         al[i] = *reinterpret_cast<const half8*>(A + A_SZ + row * PITCH + ks + kh);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int pos = (2 * wn + j + ky) * PW + l32 + kx;
+      for (int j = 0; j < TN; ++j) {
+        const int pos = (TN * wn + j + ky) * PW + l32 + kx;
         bh[j] = *reinterpret_cast<const half8*>(Bp + pos * PITCH + ks + kh);
         bl[j] = *reinterpret_cast<const half8*>(Bp + B_SZ + pos * PITCH + ks + kh);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < TN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
@@ -180,15 +197,19 @@ __global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _F
     // the weight buffer (s+1)&1 was last read in step s-1 and the patch buffer (c+1)&1 in chunk
     // c-1, both before the previous barrier
     if (more) store_a((s + 1) & 1);
-    if (pstage) store_p((c + 1) & 1, tap);
+    if (pstage) {
+#pragma unroll
+      for (int u = 0; u < G::PPT; ++u)
+        if (tap * G::PPT + u < G::PARTS) store_p((c + 1) & 1, tap * G::PPT + u, rp[u]);
+    }
     __syncthreads();
   }
 
   // ---- epilogue (C/D map: col = lane&31 = pixel column, row = Cout)
   const int khalf = lane >> 5;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int oy = oy0 + 2 * wn + j, ox = ox0 + l32;
+  for (int j = 0; j < TN; ++j) {
+    const int oy = oy0 + TN * wn + j, ox = ox0 + l32;
     if (oy >= P.Ho || ox >= P.Wo) continue;
     const int p = oy * P.Wo + ox;
 #pragma unroll
@@ -202,16 +223,30 @@ __global__ __launch_bounds__(HT) void conv3x3_halo_kernel(ConvParams P, const _F
 }
 
 bool conv_halo_ok(const ConvParams& P, int cin_pad) {
-  return P.K == 3 && P.stride == 1 && P.pad == 1 && P.nseg == 1 && P.Ho == P.H && P.Wo == P.W &&
-         cin_pad % CK == 0 && cin_pad >= P.Cin && P.Cin >= 64 && P.Cout >= 64;
+  if (!(P.K == 1 || P.K == 3 || P.K == 5) || P.stride != 1 || P.pad != P.K / 2) return false;
+  if (P.Ho != P.H || P.Wo != P.W || cin_pad % CK != 0 || cin_pad < P.Cin || P.Cin < 32 || P.Cout < 32) return false;
+  for (int s = 0; s + 1 < P.nseg; ++s)
+    if (P.seg[s].C % 16 != 0) return false;
+  return true;
 }
+
+template <int K, int TH>
+static void launch_halo(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
+  const int ntx = (P.Wo + TW - 1) / TW, nty = (P.Ho + TH - 1) / TH;
+  dim3 grid((P.Cout + HBM - 1) / HBM, ntx * nty, P.B);
+  hipLaunchKernelGGL((conv_halo_kernel<K, TH>), grid, dim3(HT), 0, st, P, wh, wl, cin_pad);
+  HIP_OK(hipGetLastError());
+}
+
+int conv_halo_tile_h(const ConvParams& P) { return P.K == 5 ? 4 : 8; }
 
 void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   MLIC_CHECK(conv_halo_ok(P, cin_pad), "conv_halo: unsupported shape");
-  const int ntx = (P.Wo + TW - 1) / TW, nty = (P.Ho + TH - 1) / TH;
-  dim3 grid((P.Cout + HBM - 1) / HBM, ntx * nty, P.B);
-  hipLaunchKernelGGL(conv3x3_halo_kernel, grid, dim3(HT), 0, st, P, wh, wl, cin_pad);
-  HIP_OK(hipGetLastError());
+  switch (P.K) {
+    case 1: launch_halo<1, 8>(P, wh, wl, cin_pad, st); break;
+    case 3: launch_halo<3, 8>(P, wh, wl, cin_pad, st); break;
+    default: launch_halo<5, 4>(P, wh, wl, cin_pad, st); break;
+  }
 }
 
 }  // namespace mlic
