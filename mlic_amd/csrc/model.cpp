@@ -675,8 +675,8 @@ void Model::lrp(const std::vector<View>& ins, const std::string& kind, int i, co
 class PhaseDecoder {
  public:
   PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym, int32_t* h_idx,
-               HostStats* hs)
-      : t_(t), h_sym_(h_sym), h_idx_(h_idx), hs_(hs) {
+               HostStats* hs, HostPool* pool)
+      : t_(t), h_sym_(h_sym), h_idx_(h_idx), hs_(hs), pool_(pool) {
     dec_.resize(B);
     for (int b = 0; b < B; ++b) dec_[b].set_stream(y[b], ylen[b]);
   }
@@ -691,13 +691,7 @@ class PhaseDecoder {
       HostStats::Scope d{hs_->dec_ns};
       dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per);
     };
-    if (B == 1) {
-      work(0);
-    } else {
-      std::vector<std::thread> th;
-      for (int b = 0; b < B; ++b) th.emplace_back(work, b);
-      for (auto& x : th) x.join();
-    }
+    pool_->run(B, work);
     HIP_OK(hipMemcpyAsync(d_sym, h_sym_, sizeof(int32_t) * n_per * B, hipMemcpyHostToDevice, st));
   }
 
@@ -707,6 +701,7 @@ class PhaseDecoder {
   int32_t* h_sym_;
   int32_t* h_idx_;
   HostStats* hs_;
+  HostPool* pool_;
 };
 
 // mlicpp.py:107-176 (forward), 220-277 (compress), 309-366 (decompress)
@@ -1064,23 +1059,17 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     for (int64_t i = 0; i < zper; ++i) zi[i] = (int32_t)(i / ((int64_t)hz * wz));
     l.enc[b].z = rans_encode(hzs + b * zper, zi.data(), zper, eb_);
   };
-  if (B == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    std::vector<std::exception_ptr> errs(B);
-    for (int b = 0; b < B; ++b)
-      th.emplace_back([&, b] {
-        try {
-          work(b);
-        } catch (...) {
-          errs[b] = std::current_exception();
-        }
-      });
-    for (auto& t : th) t.join();
-    for (auto& e : errs)
-      if (e) std::rethrow_exception(e);
-  }
+  host_pool().run(B, work);
+}
+
+HostPool& Model::host_pool() {
+  std::call_once(pool_once_, [this] {
+    int n = (int)std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("MLIC_HOST_THREADS")) n = std::atoi(e);
+    n = std::max(1, std::min(n, 16));
+    pool_ = std::make_unique<HostPool>(n);
+  });
+  return *pool_;
 }
 
 void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
@@ -1111,7 +1100,7 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
       d.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
     }
   }
-  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_);
+  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool());
   const int32_t* hz_sym = l.h_sym;
   planned(B, nullptr, [&] {
     int32_t* d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(B * zper));

@@ -10,6 +10,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "pool.h"
 #include "rans.h"
 
 namespace mlic {
@@ -122,6 +123,7 @@ class Model {
   ~Model();
   const Cfg& cfg() const { return cfg_; }
   HostStats& host_stats() { return hstats_; }
+  HostPool& host_pool();  // shared entropy-coding workers ($MLIC_HOST_THREADS, <= 16)
 
   // forward(): x [B,3,H,W] -> x_hat, y_lik [B,M,H/16,W/16], z_lik [B,N,H/64,W/64] (any may be null)
   void forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
@@ -165,6 +167,8 @@ class Model {
   int nlanes_ = 2;
   int precision_ = PREC_F16X3_V2;
   HostStats hstats_;
+  std::once_flag pool_once_;
+  std::unique_ptr<HostPool> pool_;
   bool prof_ = false;
   static thread_local Lane* tl_lane_;
   Lane& L() const { return *tl_lane_; }
