@@ -20,47 +20,56 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace mlic {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 namespace {
-constexpr int HT = 512;       // threads (8 waves: 2 along Cout x 4 along pixel rows)
-constexpr int HBM = 128;      // Cout per block
+constexpr int HT = 512;       // threads (8 waves)
 constexpr int TW = 32;        // output tile width
 constexpr int CK = 32;        // channels per chunk
 constexpr int PITCH = 40;     // halves per LDS row (32 + 8): conflict-free b128 reads
-constexpr int A_SZ = HBM * PITCH;
-constexpr int A_BUF = 2 * A_SZ;
 
-template <int K, int TH>
+// BM = Cout per block.  BM = 128: 2 x 4 waves of 64 Cout x (TH/4 rows x 32 px), double-buffered
+// patch.  BM = 256: 4 x 2 waves of 64 Cout x (TH/2 rows x 32 px) — twice the MFMAs per fragment
+// read (the split-fp16 kernels read hi and lo of both operands, so the 64 x 64 wave tile is
+// LDS-bandwidth-bound) — with a single patch buffer refilled from registers at chunk boundaries.
+template <int K, int TH, int BM>
 struct Halo {
   static constexpr int KK = K * K;
+  static constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
+  static constexpr int TN = TH / WAVES_N;                    // pixel rows per wave
+  static constexpr bool PATCH_DB = BM == 128;
+  static constexpr int A_SZ = BM * PITCH, A_BUF = 2 * A_SZ;
   static constexpr int PH = TH + K - 1, PW = TW + K - 1, NPOS = PH * PW;
   static constexpr int B_SZ = NPOS * PITCH, B_BUF = 2 * B_SZ;
-  static constexpr int LDS_HALVES = 2 * A_BUF + 2 * B_BUF;
+  static constexpr int LDS_HALVES = 2 * A_BUF + (PATCH_DB ? 2 : 1) * B_BUF;
   static constexpr int PITEMS = NPOS * (CK / 8);            // staging items: 8 channels at one position
   static constexpr int PARTS = (PITEMS + HT - 1) / HT;       // items per thread per chunk
-  static constexpr int PPT = (PARTS + KK - 1) / KK;          // parts loaded per tap
-  static constexpr int TN = TH / 4;                          // pixel rows per wave
+  static constexpr int PPT = PATCH_DB ? (PARTS + KK - 1) / KK : PARTS;  // parts held per load tap
+  static constexpr int ACH = BM * CK / 8 / HT;               // 16-byte weight chunks per thread
   static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
-  static_assert(TH % 4 == 0, "tile");
+  static_assert(TH % WAVES_N == 0 && ACH >= 1, "tile");
+  static_assert(PATCH_DB || KK > 1, "single patch buffer needs a later tap to write it");
 };
 }  // namespace
 
-template <int K, int TH>
+template <int K, int TH, int BM>
 __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Float16* __restrict__ wh,
                                                        const _Float16* __restrict__ wl, int cin_pad) {
-  using G = Halo<K, TH>;
+  using G = Halo<K, TH, BM>;
   constexpr int KK = G::KK, PW = G::PW, NPOS = G::NPOS, B_SZ = G::B_SZ, B_BUF = G::B_BUF, TN = G::TN;
+  constexpr int A_SZ = G::A_SZ, A_BUF = G::A_BUF, HBM = BM;
   __shared__ __attribute__((aligned(16))) _Float16 sm[G::LDS_HALVES];
-  _Float16* As = sm;                  // [2][hi|lo][HBM][PITCH]
-  _Float16* Bs = sm + 2 * A_BUF;      // [2][hi|lo][NPOS][PITCH]
+  _Float16* As = sm;                  // [2][hi|lo][BM][PITCH]
+  _Float16* Bs = sm + 2 * A_BUF;      // [1 or 2][hi|lo][NPOS][PITCH]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / G::WAVES_N, wn = wave % G::WAVES_N;
 
   // block -> (Cout tile, spatial tile), XCD-aware bijective remap as conv_x3v2
   const int ntx = (P.Wo + TW - 1) / TW, nty = (P.Ho + TH - 1) / TH;
@@ -82,27 +91,35 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
   const bool square = (P.epi & EPI_SQUARE_IN) != 0;
 
   // ---- staging helpers
-  uint4 ra_h, ra_l;  // one 16-byte chunk of the hi and lo weight tile per thread
+  uint4 ra_h[G::ACH], ra_l[G::ACH];  // 16-byte chunks of the hi and lo weight tile
   auto load_a = [&](int s) {
     const int c = s / KK, tap = s - KK * (s / KK);
-    const int row = tid >> 2, q = tid & 3;
-    const int co = co0 + row;
-    if (co < P.Cout) {
-      const int64_t off = ((int64_t)co * KK + tap) * cin_pad + c * CK + 8 * q;
-      ra_h = *reinterpret_cast<const uint4*>(wh + off);
-      ra_l = *reinterpret_cast<const uint4*>(wl + off);
-    } else {
-      ra_h = make_uint4(0, 0, 0, 0);
-      ra_l = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < G::ACH; ++u) {
+      const int id = tid + u * HT;
+      const int row = id >> 2, q = id & 3;
+      const int co = co0 + row;
+      if (co < P.Cout) {
+        const int64_t off = ((int64_t)co * KK + tap) * cin_pad + c * CK + 8 * q;
+        ra_h[u] = *reinterpret_cast<const uint4*>(wh + off);
+        ra_l[u] = *reinterpret_cast<const uint4*>(wl + off);
+      } else {
+        ra_h[u] = make_uint4(0, 0, 0, 0);
+        ra_l[u] = make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto store_a = [&](int buf) {
-    const int row = tid >> 2, q = tid & 3;
     _Float16* base = As + buf * A_BUF;
-    *reinterpret_cast<uint4*>(base + row * PITCH + 8 * q) = ra_h;
-    *reinterpret_cast<uint4*>(base + A_SZ + row * PITCH + 8 * q) = ra_l;
+#pragma unroll
+    for (int u = 0; u < G::ACH; ++u) {
+      const int id = tid + u * HT;
+      const int row = id >> 2, q = id & 3;
+      *reinterpret_cast<uint4*>(base + row * PITCH + 8 * q) = ra_h[u];
+      *reinterpret_cast<uint4*>(base + A_SZ + row * PITCH + 8 * q) = ra_l[u];
+    }
   };
-  float rp[G::PPT][8];  // 8 channels of one patch position, per part
+  float rp[G::PPT][8];  // 8 channels of one patch position, per part held in registers
   auto load_p = [&](int c, int part, float (&dst)[8]) {
     const int item = part * HT + tid;
     if (item >= G::PITEMS) return;
@@ -160,16 +177,21 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
     const int c = s / KK, tap = s - KK * c;
     const int ky = tap / K, kx = tap - K * ky;
     const bool more = s + 1 < nsteps;
-    const bool pstage = (c + 1 < nchunk) && tap * G::PPT < G::PARTS;
+    const bool next_chunk = c + 1 < nchunk;
     if (more) load_a(s + 1);
-    if (pstage) {
+    if constexpr (G::PATCH_DB) {
+      if (next_chunk && tap * G::PPT < G::PARTS) {
 #pragma unroll
-      for (int u = 0; u < G::PPT; ++u)
-        if (tap * G::PPT + u < G::PARTS) load_p(c + 1, tap * G::PPT + u, rp[u]);
+        for (int u = 0; u < G::PPT; ++u)
+          if (tap * G::PPT + u < G::PARTS) load_p(c + 1, tap * G::PPT + u, rp[u]);
+      }
+    } else if (next_chunk && tap == 0) {  // held in registers until the chunk's last tap
+#pragma unroll
+      for (int u = 0; u < G::PARTS; ++u) load_p(c + 1, u, rp[u]);
     }
 
     const _Float16* A = As + (s & 1) * A_BUF;
-    const _Float16* Bp = Bs + (c & 1) * B_BUF;
+    const _Float16* Bp = Bs + (G::PATCH_DB ? (c & 1) * B_BUF : 0);
 #pragma unroll
     for (int ks = 0; ks < CK; ks += 16) {
       half8 ah[2], al[2], bh[TN], bl[TN];
@@ -197,10 +219,16 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
     // the weight buffer (s+1)&1 was last read in step s-1 and the patch buffer (c+1)&1 in chunk
     // c-1, both before the previous barrier
     if (more) store_a((s + 1) & 1);
-    if (pstage) {
+    if constexpr (G::PATCH_DB) {
+      if (next_chunk && tap * G::PPT < G::PARTS) {
 #pragma unroll
-      for (int u = 0; u < G::PPT; ++u)
-        if (tap * G::PPT + u < G::PARTS) store_p((c + 1) & 1, tap * G::PPT + u, rp[u]);
+        for (int u = 0; u < G::PPT; ++u)
+          if (tap * G::PPT + u < G::PARTS) store_p((c + 1) & 1, tap * G::PPT + u, rp[u]);
+      }
+    } else if (next_chunk && tap == KK - 1) {
+      __syncthreads();  // every wave is done with this chunk's patch
+#pragma unroll
+      for (int u = 0; u < G::PARTS; ++u) store_p(0, u, rp[u]);
     }
     __syncthreads();
   }
@@ -230,22 +258,32 @@ bool conv_halo_ok(const ConvParams& P, int cin_pad) {
   return true;
 }
 
-template <int K, int TH>
+template <int K, int TH, int BM>
 static void launch_halo(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   const int ntx = (P.Wo + TW - 1) / TW, nty = (P.Ho + TH - 1) / TH;
-  dim3 grid((P.Cout + HBM - 1) / HBM, ntx * nty, P.B);
-  hipLaunchKernelGGL((conv_halo_kernel<K, TH>), grid, dim3(HT), 0, st, P, wh, wl, cin_pad);
+  dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B);
+  hipLaunchKernelGGL((conv_halo_kernel<K, TH, BM>), grid, dim3(HT), 0, st, P, wh, wl, cin_pad);
   HIP_OK(hipGetLastError());
 }
 
-int conv_halo_tile_h(const ConvParams& P) { return P.K == 5 ? 4 : 8; }
+// $MLIC_HALO_WIDE=0 keeps the 128-row tiles for every shape (A/B switch)
+static bool halo_wide() {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_HALO_WIDE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 
 void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   MLIC_CHECK(conv_halo_ok(P, cin_pad), "conv_halo: unsupported shape");
   switch (P.K) {
-    case 1: launch_halo<1, 8>(P, wh, wl, cin_pad, st); break;
-    case 3: launch_halo<3, 8>(P, wh, wl, cin_pad, st); break;
-    default: launch_halo<5, 4>(P, wh, wl, cin_pad, st); break;
+    case 1: launch_halo<1, 8, 128>(P, wh, wl, cin_pad, st); break;
+    case 3:
+      if (P.Cout > 128 && halo_wide()) launch_halo<3, 8, 256>(P, wh, wl, cin_pad, st);
+      else launch_halo<3, 8, 128>(P, wh, wl, cin_pad, st);
+      break;
+    default: launch_halo<5, 4, 128>(P, wh, wl, cin_pad, st); break;
   }
 }
 
