@@ -22,7 +22,10 @@ int conv_prof_cat(int impl, const ConvParams& P) {
   switch (impl) {
     case CONV_F32: return PCAT_CONV_F32 + conv_variant(P);
     case CONV_X3: return PCAT_CONV_X3 + conv_f16x3_variant(P);
-    case CONV_X3V2: return PCAT_CONV_X3V2 + std::min(conv_x3v2_variant(P), 2);
+    case CONV_X3V2: {
+      const int v = conv_x3v2_variant(P);
+      return v == 3 ? PCAT_CONV_X3V2_WIDE : PCAT_CONV_X3V2 + v;
+    }
     case CONV_PW: return PCAT_CONV_PW;
     case CONV_NARROW: return PCAT_CONV_NARROW;
     case CONV_HALO: return PCAT_CONV_HALO;
@@ -48,7 +51,8 @@ const char* prof_cat_name(int cat) {
       "conv_mfma_kernel<64,64>",     "conv_mfma_kernel<64,128>",  "conv_mfma_kernel<128,64>",
       "conv_mfma_kernel<128,128>",   "conv_f16x3_kernel<32,256>", "conv_f16x3_kernel<64,128>",
       "conv_f16x3_kernel<128,64>",   "conv_f16x3_kernel<128,128>", "conv_x3v2_kernel<64,128>",
-      "conv_x3v2_kernel<128,256>",   "conv_x3v2_kernel<128,128>", "pw_resident_kernel",
+      "conv_x3v2_kernel<128,256>",   "conv_x3v2_kernel<128,128>", "conv_x3v2_kernel<256,256>",
+      "pw_resident_kernel",
       "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "conv_halo_kernel",
       "dw3x3_kernel",
       "local_attn_kernel",           "linear_attention",          "elementwise"};

@@ -15,6 +15,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace mlic {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -252,6 +254,15 @@ void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16*
 }
 
 
+// $MLIC_V2_WIDE=1 selects the 8-wave 256x256 tile for large-Cout GEMMs (experimental)
+static bool v2_wide() {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_V2_WIDE");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // ---------------------------------------------------------------------------------------------
 // v2: B (activations) staged in its natural [k][n] orientation — float4 loads along pixels for
 // 1x1 convs, 4-pixel strips otherwise, conflict-free ds_write_b64 of the hi/lo halves — and the
@@ -268,14 +279,15 @@ __device__ __forceinline__ half8 tr_read8(const _Float16* p0, const _Float16* p1
   return __builtin_bit_cast(half8, c);
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(XB_THREADS) void conv_x3v2_kernel(ConvParams P, const _Float16* __restrict__ wh,
-                                                                const _Float16* __restrict__ wl, int cin_pad) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+template <int BM, int BN, int WAVES_M = 2, int WAVES_N = 2>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvParams P, const _Float16* __restrict__ wh,
+                                                                            const _Float16* __restrict__ wl, int cin_pad) {
+  constexpr int XT = 64 * WAVES_M * WAVES_N;  // threads
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_CHUNKS = BM * XB_K / 8 / XB_THREADS;
+  constexpr int A_CHUNKS = BM * XB_K / 8 / XT;
   constexpr int QN = BN / 4;                 // pixel quads per k row
-  constexpr int RPT = XB_K * QN / XB_THREADS;  // k rows staged per thread
+  constexpr int RPT = XB_K * QN / XT;  // k rows staged per thread
   static_assert(A_CHUNKS >= 1 && RPT >= 1 && RPT <= 16, "tile");
   constexpr int APITCH = XB_PITCH;           // halves
   constexpr int BPITCH = BN + 32;            // halves
@@ -286,7 +298,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_x3v2_kernel(ConvParams P, con
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int nct = gridDim.x, npt = gridDim.y, nblk = nct * npt;
   const int bid = blockIdx.y * nct + blockIdx.x;
   int logical = bid;
@@ -325,7 +337,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_x3v2_kernel(ConvParams P, con
     const int c0 = (t - tap * nck) * XB_K;
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
-      const int id = tid + i * XB_THREADS;
+      const int id = tid + i * XT;
       const int row = id >> 2, qq = id & 3;
       const int co = co0 + row;
       if (co < P.Cout) {
@@ -380,7 +392,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_x3v2_kernel(ConvParams P, con
     _Float16* base = sm + buf * BUF;
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
-      const int id = tid + i * XB_THREADS;
+      const int id = tid + i * XT;
       const int row = id >> 2, qq = id & 3;
       *reinterpret_cast<uint4*>(base + row * APITCH + 8 * qq) = ra_h[i];
       *reinterpret_cast<uint4*>(base + A_SZ + row * APITCH + 8 * qq) = ra_l[i];
@@ -491,19 +503,23 @@ __global__ __launch_bounds__(XB_THREADS) void conv_x3v2_kernel(ConvParams P, con
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WAVES_M = 2, int WAVES_N = 2>
 static void launch_v2(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   const int HWo = P.Ho * P.Wo;
   dim3 grid((P.Cout + BM - 1) / BM, (HWo + BN - 1) / BN, P.B);
-  hipLaunchKernelGGL((conv_x3v2_kernel<BM, BN>), grid, dim3(XB_THREADS), 0, st, P, wh, wl, cin_pad);
+  hipLaunchKernelGGL((conv_x3v2_kernel<BM, BN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N), 0, st, P, wh,
+                     wl, cin_pad);
   HIP_OK(hipGetLastError());
 }
 
+// 0 <64,128>, 1 <128,256>, 2 <128,128>, 3 <256,256> (8 waves of 64 x 128: twice the MFMAs per
+// LDS fragment read of the 64 x 64 wave tiles, which are LDS-bandwidth-bound in split-fp16)
 int conv_x3v2_variant(const ConvParams& P) {
   const int64_t HWo = (int64_t)P.Ho * P.Wo;
-  if (P.Cout <= 64) return 0;                     // <64,128>
-  if (P.Cout <= 192 && HWo >= 128 * 512) return 1;  // <128,256> wide pixel tiles for mid-Cout layers
-  return HWo >= 128 * 512 ? 3 : 2;                // <128,128> / <128,128>
+  if (P.Cout <= 64) return 0;
+  if (P.Cout <= 192 && HWo >= 128 * 512) return 1;
+  if (P.Cout >= 192 && HWo * P.B >= 8192 && v2_wide()) return 3;
+  return 2;
 }
 
 void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
@@ -512,6 +528,7 @@ void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
   switch (conv_x3v2_variant(P)) {
     case 0: launch_v2<64, 128>(P, wh, wl, cin_pad, st); break;
     case 1: launch_v2<128, 256>(P, wh, wl, cin_pad, st); break;
+    case 3: launch_v2<256, 256, 4, 2>(P, wh, wl, cin_pad, st); break;
     default: launch_v2<128, 128>(P, wh, wl, cin_pad, st); break;
   }
 }

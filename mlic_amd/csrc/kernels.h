@@ -47,16 +47,17 @@ void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t s
 enum ProfCat : int {
   PCAT_CONV_F32 = 0,     // 0..3  conv_mfma_kernel tiles (conv_variant)
   PCAT_CONV_X3 = 4,      // 4..7  conv_f16x3_kernel tiles (conv_f16x3_variant)
-  PCAT_CONV_X3V2 = 8,    // 8..10 conv_x3v2_kernel tiles
-  PCAT_CONV_PW = 11,
-  PCAT_CONV_NARROW = 12,
-  PCAT_CONV_SMALLCIN = 13,
-  PCAT_CONV_HALO = 14,
-  PCAT_DW = 15,
-  PCAT_LOCAL = 16,
-  PCAT_LINATT = 17,
-  PCAT_ELEM = 18,
-  PCAT_COUNT = 19
+  PCAT_CONV_X3V2 = 8,    // 8..10 conv_x3v2_kernel tiles <64,128>, <128,256>, <128,128>
+  PCAT_CONV_X3V2_WIDE = 11,  // conv_x3v2_kernel<256,256> (8 waves)
+  PCAT_CONV_PW = 12,
+  PCAT_CONV_NARROW = 13,
+  PCAT_CONV_SMALLCIN = 14,
+  PCAT_CONV_HALO = 15,
+  PCAT_DW = 16,
+  PCAT_LOCAL = 17,
+  PCAT_LINATT = 18,
+  PCAT_ELEM = 19,
+  PCAT_COUNT = 20
 };
 int conv_prof_cat(int impl, const ConvParams& P);
 const char* prof_cat_name(int cat);
