@@ -11,8 +11,9 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (precision == 1) return CONV_X3;
   // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
   if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
-  // halo 3x3: enough 128 x 256 tiles to fill the chip
-  if (P.K == 3 && conv_halo_ok(P, w.cin_pad) &&
+  // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
+  // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay
+  if (P.K == 5 && conv_halo_ok(P, w.cin_pad) &&
       (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 7) / 8) * P.B >= 256)
     return CONV_HALO;
   return CONV_X3V2;

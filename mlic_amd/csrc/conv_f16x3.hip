@@ -254,11 +254,11 @@ void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16*
 }
 
 
-// $MLIC_V2_WIDE=1 selects the 8-wave 256x256 tile for large-Cout GEMMs (experimental)
+// $MLIC_V2_WIDE=0 disables the 8-wave 256x256 tile (A/B switch)
 static bool v2_wide() {
   static const bool on = [] {
     const char* e = std::getenv("MLIC_V2_WIDE");
-    return e && std::atoi(e) != 0;
+    return !(e && std::atoi(e) == 0);
   }();
   return on;
 }
@@ -513,12 +513,15 @@ static void launch_v2(const ConvParams& P, const _Float16* wh, const _Float16* w
 }
 
 // 0 <64,128>, 1 <128,256>, 2 <128,128>, 3 <256,256> (8 waves of 64 x 128: twice the MFMAs per
-// LDS fragment read of the 64 x 64 wave tiles, which are LDS-bandwidth-bound in split-fp16)
+// LDS fragment read of the 64 x 64 wave tiles, which are LDS-bandwidth-bound in split-fp16;
+// measured 244 vs 184 TF/s on the g_s subpel conv).  The wide tile is used where its 256-row
+// Cout tiles are at least 3/4 occupied (Cout 192..256, 384..512, 576..768, ...).
 int conv_x3v2_variant(const ConvParams& P) {
   const int64_t HWo = (int64_t)P.Ho * P.Wo;
   if (P.Cout <= 64) return 0;
+  const int ct = (P.Cout + 255) / 256;
+  if (v2_wide() && P.Cout >= 192 && 4 * P.Cout >= 3 * 256 * ct && HWo * P.B >= 8192) return 3;
   if (P.Cout <= 192 && HWo >= 128 * 512) return 1;
-  if (P.Cout >= 192 && HWo * P.B >= 8192 && v2_wide()) return 3;
   return 2;
 }
 

@@ -34,9 +34,8 @@ constexpr int CK = 32;        // channels per chunk
 constexpr int PITCH = 40;     // halves per LDS row (32 + 8): conflict-free b128 reads
 
 // BM = Cout per block.  BM = 128: 2 x 4 waves of 64 Cout x (TH/4 rows x 32 px), double-buffered
-// patch.  BM = 256: 4 x 2 waves of 64 Cout x (TH/2 rows x 32 px) — twice the MFMAs per fragment
-// read (the split-fp16 kernels read hi and lo of both operands, so the 64 x 64 wave tile is
-// LDS-bandwidth-bound) — with a single patch buffer refilled from registers at chunk boundaries.
+// patch.  (A BM = 256 form — 64 x 128 wave tiles, single patch buffer refilled from registers —
+// needs > 256 VGPRs at 2 waves/SIMD and spills; measured 2.7x slower, so only 128 is built.)
 template <int K, int TH, int BM>
 struct Halo {
   static constexpr int KK = K * K;
@@ -173,64 +172,72 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
   __syncthreads();
 
   const int l32 = lane & 31, kh = (lane >> 5) * 8;
-  for (int s = 0; s < nsteps; ++s) {
-    const int c = s / KK, tap = s - KK * c;
-    const int ky = tap / K, kx = tap - K * ky;
-    const bool more = s + 1 < nsteps;
+  // chunk loop with the taps unrolled: tap, ky, kx and every staging decision are compile-time,
+  // and every barrier is unconditional (a data-dependent barrier made hipcc keep the
+  // accumulators in scratch)
+  for (int c = 0; c < nchunk; ++c) {
     const bool next_chunk = c + 1 < nchunk;
-    if (more) load_a(s + 1);
-    if constexpr (G::PATCH_DB) {
-      if (next_chunk && tap * G::PPT < G::PARTS) {
-#pragma unroll
-        for (int u = 0; u < G::PPT; ++u)
-          if (tap * G::PPT + u < G::PARTS) load_p(c + 1, tap * G::PPT + u, rp[u]);
-      }
-    } else if (next_chunk && tap == 0) {  // held in registers until the chunk's last tap
-#pragma unroll
-      for (int u = 0; u < G::PARTS; ++u) load_p(c + 1, u, rp[u]);
-    }
-
-    const _Float16* A = As + (s & 1) * A_BUF;
     const _Float16* Bp = Bs + (G::PATCH_DB ? (c & 1) * B_BUF : 0);
 #pragma unroll
-    for (int ks = 0; ks < CK; ks += 16) {
-      half8 ah[2], al[2], bh[TN], bl[TN];
+    for (int tap = 0; tap < KK; ++tap) {
+      const int s = c * KK + tap;
+      const int ky = tap / K, kx = tap - K * (tap / K);
+      const bool more = s + 1 < nsteps;
+      if (more) load_a(s + 1);
+      if constexpr (G::PATCH_DB) {
+        if (tap * G::PPT < G::PARTS && next_chunk) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wm * 64 + i * 32 + l32;
-        ah[i] = *reinterpret_cast<const half8*>(A + row * PITCH + ks + kh);
-        al[i] = *reinterpret_cast<const half8*>(A + A_SZ + row * PITCH + ks + kh);
+          for (int u = 0; u < G::PPT; ++u)
+            if (tap * G::PPT + u < G::PARTS) load_p(c + 1, tap * G::PPT + u, rp[u]);
+        }
+      } else if (tap == 0 && next_chunk) {  // held in registers until the chunk's last tap
+#pragma unroll
+        for (int u = 0; u < G::PARTS; ++u) load_p(c + 1, u, rp[u]);
       }
+
+      const _Float16* A = As + (s & 1) * A_BUF;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int pos = (TN * wn + j + ky) * PW + l32 + kx;
-        bh[j] = *reinterpret_cast<const half8*>(Bp + pos * PITCH + ks + kh);
-        bl[j] = *reinterpret_cast<const half8*>(Bp + B_SZ + pos * PITCH + ks + kh);
-      }
+      for (int ks = 0; ks < CK; ks += 16) {
+        half8 ah[2], al[2], bh[TN], bl[TN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i) {
+          const int row = wm * 64 + i * 32 + l32;
+          ah[i] = *reinterpret_cast<const half8*>(A + row * PITCH + ks + kh);
+          al[i] = *reinterpret_cast<const half8*>(A + A_SZ + row * PITCH + ks + kh);
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          const int pos = (TN * wn + j + ky) * PW + l32 + kx;
+          bh[j] = *reinterpret_cast<const half8*>(Bp + pos * PITCH + ks + kh);
+          bl[j] = *reinterpret_cast<const half8*>(Bp + B_SZ + pos * PITCH + ks + kh);
         }
-    }
-    // the weight buffer (s+1)&1 was last read in step s-1 and the patch buffer (c+1)&1 in chunk
-    // c-1, both before the previous barrier
-    if (more) store_a((s + 1) & 1);
-    if constexpr (G::PATCH_DB) {
-      if (next_chunk && tap * G::PPT < G::PARTS) {
 #pragma unroll
-        for (int u = 0; u < G::PPT; ++u)
-          if (tap * G::PPT + u < G::PARTS) store_p((c + 1) & 1, tap * G::PPT + u, rp[u]);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
       }
-    } else if (next_chunk && tap == KK - 1) {
-      __syncthreads();  // every wave is done with this chunk's patch
+      // the weight buffer (s+1)&1 was last read in step s-1 and the patch buffer (c+1)&1 in chunk
+      // c-1, both before the previous barrier
+      if (more) store_a((s + 1) & 1);
+      if constexpr (G::PATCH_DB) {
+        if (tap * G::PPT < G::PARTS && next_chunk) {
 #pragma unroll
-      for (int u = 0; u < G::PARTS; ++u) store_p(0, u, rp[u]);
+          for (int u = 0; u < G::PPT; ++u)
+            if (tap * G::PPT + u < G::PARTS) store_p((c + 1) & 1, tap * G::PPT + u, rp[u]);
+        }
+      } else if (tap == KK - 1) {
+        __syncthreads();  // every wave is done with this chunk's patch (uniform: tap is static)
+        if (next_chunk) {
+#pragma unroll
+          for (int u = 0; u < G::PARTS; ++u) store_p(0, u, rp[u]);
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 
   // ---- epilogue (C/D map: col = lane&31 = pixel column, row = Cout)
@@ -266,23 +273,11 @@ static void launch_halo(const ConvParams& P, const _Float16* wh, const _Float16*
   HIP_OK(hipGetLastError());
 }
 
-// $MLIC_HALO_WIDE=1 selects the 256-row tiles for Cout > 128 (measured 2.7x slower on g_s.5: off)
-static bool halo_wide() {
-  static const bool on = [] {
-    const char* e = std::getenv("MLIC_HALO_WIDE");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
 void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   MLIC_CHECK(conv_halo_ok(P, cin_pad), "conv_halo: unsupported shape");
   switch (P.K) {
     case 1: launch_halo<1, 8, 128>(P, wh, wl, cin_pad, st); break;
-    case 3:
-      if (P.Cout > 128 && halo_wide()) launch_halo<3, 8, 256>(P, wh, wl, cin_pad, st);
-      else launch_halo<3, 8, 128>(P, wh, wl, cin_pad, st);
-      break;
+    case 3: launch_halo<3, 8, 128>(P, wh, wl, cin_pad, st); break;
     default: launch_halo<5, 4, 128>(P, wh, wl, cin_pad, st); break;
   }
 }

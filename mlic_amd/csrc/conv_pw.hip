@@ -18,8 +18,8 @@
 // 2. conv3x3_narrow_kernel — 3x3 stride-1 convs with Cout <= 16 (g_s's last subpel conv, N -> 12).
 //    On MFMA a 12-row output wastes >80 % of a 64-row tile; as a direct convolution on the fp32
 //    VALU (exact fp32, packed 2-pixel FMAs) it needs 12*9 FMAs per input value, with a 16x32 output
-//    tile's input patch (+1 halo) staged through LDS in 8-channel chunks and weights read as
-//    wave-uniform scalars.
+//    tile's input patch (+1 halo) and the chunk's weights (as duplicated pairs, read by broadcast
+//    ds_read_b128 straight into v_pk_fma_f32 operands) staged through LDS in 8-channel chunks.
 //
 // 3. conv1x1_smallcin_kernel — 1x1 convs with Cin <= 4 (g_a's first point conv and skip, 3 -> N):
 //    write-bound; one pixel per lane, Cout outputs from scalar weights.
@@ -309,7 +309,13 @@ constexpr int NR_STAGE = (NR_PATCH + 255) / 256;
 template <int COUT>
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
   typedef float float2v __attribute__((ext_vector_type(2)));
+  typedef float float4v __attribute__((ext_vector_type(4)));
+  // per chunk: the input patch and the chunk's weights as duplicated (w, w) pairs, so one
+  // broadcast ds_read_b128 yields the packed operands of two v_pk_fma_f32 (2 pixels x 2 Cout)
+  constexpr int NW = NR_CC * 9 * COUT;  // weights per chunk
+  static_assert(COUT % 2 == 0, "Cout pairs");
   __shared__ __attribute__((aligned(16))) float sm[2 * NR_PATCH];
+  __shared__ __attribute__((aligned(16))) float4v swp[2][NW / 2];  // [c][tap][co pair] -> (w0, w0, w1, w1)
   const int tid = threadIdx.x;
   const int tx = tid & 15, ty = tid >> 4;  // 2 output pixels (2tx, 2tx+1) of row ty
   const int ow0 = blockIdx.x * NR_TW, oh0 = blockIdx.y * NR_TH;
@@ -318,8 +324,11 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
   const int64_t HW = (int64_t)H * W;
   const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs;
   const int nchunk = (P.Cin + NR_CC - 1) / NR_CC;
+  const float* w = P.wpk;  // [9][Cin][COUT]
+  constexpr int WSTAGE = (NW / 2 + 255) / 256;
 
   float stage[NR_STAGE];
+  float4v wst[WSTAGE];
   auto load = [&](int ch) {
 #pragma unroll
     for (int s = 0; s < NR_STAGE; ++s) {
@@ -335,12 +344,32 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
       }
       stage[s] = v;
     }
+#pragma unroll
+    for (int s = 0; s < WSTAGE; ++s) {
+      const int e = tid + s * 256;  // (c, tap, co pair)
+      float4v v = {0.f, 0.f, 0.f, 0.f};
+      if (e < NW / 2) {
+        const int c = e / (9 * COUT / 2), rem = e - c * (9 * COUT / 2);
+        const int tap = rem / (COUT / 2), cp = rem - tap * (COUT / 2);
+        const int ci = ch * NR_CC + c;
+        if (ci < P.Cin) {
+          const float* wr = w + ((int64_t)tap * P.Cin + ci) * COUT + 2 * cp;
+          v = float4v{wr[0], wr[0], wr[1], wr[1]};
+        }
+      }
+      wst[s] = v;
+    }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < NR_STAGE; ++s) {
       const int e = tid + s * 256;
       if (e < NR_PATCH) sm[buf * NR_PATCH + e] = stage[s];
+    }
+#pragma unroll
+    for (int s = 0; s < WSTAGE; ++s) {
+      const int e = tid + s * 256;
+      if (e < NW / 2) swp[buf][e] = wst[s];
     }
   };
 
@@ -351,14 +380,12 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
   load(0);
   store(0);
   __syncthreads();
-  const float* w = P.wpk;  // [9][Cin][COUT]
   for (int ch = 0; ch < nchunk; ++ch) {
     const int cur = ch & 1;
     if (ch + 1 < nchunk) load(ch + 1);
     const float* pb = sm + cur * NR_PATCH + ty * NR_PW + 2 * tx;
     const int cmax = min(NR_CC, P.Cin - ch * NR_CC);
     for (int c = 0; c < cmax; ++c) {
-      const int ci = ch * NR_CC + c;
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
         const float2v x01 = *reinterpret_cast<const float2v*>(pb + c * NR_PH * NR_PW + dy * NR_PW);
@@ -366,9 +393,13 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
         const float2v xs[3] = {x01, float2v{x01.y, x23.x}, x23};
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
-          const float* wr = w + ((int64_t)(dy * 3 + dx) * P.Cin + ci) * COUT;
+          const float4v* wq = &swp[cur][(c * 9 + dy * 3 + dx) * (COUT / 2)];
 #pragma unroll
-          for (int co = 0; co < COUT; ++co) acc[co] = __builtin_elementwise_fma(xs[dx], float2v{wr[co], wr[co]}, acc[co]);
+          for (int cp = 0; cp < COUT / 2; ++cp) {
+            const float4v ww = wq[cp];  // all lanes read the same address: broadcast
+            acc[2 * cp] = __builtin_elementwise_fma(xs[dx], float2v{ww.x, ww.y}, acc[2 * cp]);
+            acc[2 * cp + 1] = __builtin_elementwise_fma(xs[dx], float2v{ww.z, ww.w}, acc[2 * cp + 1]);
+          }
         }
       }
     }
