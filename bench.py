@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=24, help="images per GPU per step")
     ap.add_argument("--model", default="MLICPP_L")
     ap.add_argument("--height", type=int, default=1088)
     ap.add_argument("--width", type=int, default=1920)
@@ -65,6 +65,9 @@ def parse():
                          "1 = f16x3 v1 tiles, 0 = fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers-out", default="", help="write the per-layer conv timing table here")
+    ap.add_argument("--profile-lanes", type=int, default=0,
+                    help="lanes of the profiled step (0 = same as --lanes, so its launches match the timed "
+                         "steps' and rocprofv3's per-kernel averages; 1 = isolated per-kernel times)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per conv launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -183,7 +186,8 @@ def main():
 
     # live roofline of the dominant kernel family: one extra profiled (untimed) step
     h = net._handle
-    _lib.call("mlic_set_lanes", h, 1)  # events on overlapping lanes would double-count device time
+    prof_lanes = a.profile_lanes or a.lanes
+    _lib.call("mlic_set_lanes", h, prof_lanes)
     _lib.call("mlic_set_profiling", h, 1)
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
@@ -282,9 +286,11 @@ def main():
                          "algorithmic_flops_per_launch": round(conv["flops"] / max(1, conv["launches"])),
                          "algorithmic_bytes_per_launch": round(conv["bytes"] / max(1, conv["launches"])),
                          "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3)},
+            # with profile_lanes > 1 these are per-launch durations summed over concurrently running lanes
             "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
             "gpu_kernel_ms_by_phase": phase_gpu,
+            "profile_lanes": prof_lanes,
             "host_thread_ms_per_step": host,
             "wall_ms_per_step": wall_split,
             "lanes": a.lanes,

@@ -14,7 +14,7 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay
   if (P.K == 5 && conv_halo_ok(P, w.cin_pad) &&
-      (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 7) / 8) * P.B >= 256)
+      (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 3) / 4) * P.B >= 64)
     return CONV_HALO;
   return CONV_X3V2;
 }
