@@ -525,10 +525,36 @@ int conv_x3v2_variant(const ConvParams& P) {
   return 2;
 }
 
+// rows [r0, r0 + n) of a conv as a conv of its own (weights, bias, output, aux and residual shifted)
+static ConvParams cout_slice(const ConvParams& P, int r0, int n) {
+  ConvParams Q = P;
+  const int64_t HWo = (int64_t)P.Ho * P.Wo;
+  const int64_t oc = (P.epi & EPI_SHUFFLE) ? (int64_t)(r0 >> 2) * P.out_cs : (int64_t)r0 * P.out_cs;
+  Q.Cout = n;
+  Q.out = P.out + oc;
+  if (P.bias) Q.bias = P.bias + r0;
+  if (P.aux) Q.aux = P.aux + (int64_t)r0 * HWo;
+  if (P.res) Q.res = P.res + oc;
+  return Q;
+}
+
 void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   MLIC_CHECK(cin_pad % XB_K == 0 && cin_pad >= P.Cin, "f16x3: padded Cin");
   for (int s = 0; s + 1 < P.nseg; ++s) MLIC_CHECK(P.seg[s].C % 16 == 0, "f16x3: segments must be 16-aligned");
-  switch (conv_x3v2_variant(P)) {
+  const int v = conv_x3v2_variant(P);
+  const int64_t HWo = (int64_t)P.Ho * P.Wo;
+  // Cout = 256k + r with r <= 128 (e.g. the entropy-parameters 640 -> 320 layer): the 256-row tiles
+  // take 256k rows and a narrow tile the remainder, instead of 128-row tiles for everything
+  const int r0 = 256 * (P.Cout / 256), rem = P.Cout - r0;
+  if (v == 2 && v2_wide() && r0 > 0 && rem > 0 && rem <= 128 && HWo * P.B >= 8192 && (r0 & 3) == 0) {
+    const int64_t wofs = (int64_t)r0 * P.K * P.K * cin_pad;
+    launch_v2<256, 256, 4, 2>(cout_slice(P, 0, r0), wh, wl, cin_pad, st);
+    const ConvParams Q = cout_slice(P, r0, rem);
+    if (rem <= 64) launch_v2<64, 128>(Q, wh + wofs, wl + wofs, cin_pad, st);
+    else launch_v2<128, 128>(Q, wh + wofs, wl + wofs, cin_pad, st);
+    return;
+  }
+  switch (v) {
     case 0: launch_v2<64, 128>(P, wh, wl, cin_pad, st); break;
     case 1: launch_v2<128, 256>(P, wh, wl, cin_pad, st); break;
     case 3: launch_v2<256, 256, 4, 2>(P, wh, wl, cin_pad, st); break;

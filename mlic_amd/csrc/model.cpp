@@ -207,13 +207,16 @@ Lane& Model::lane(int i) {
     // staggered priorities (lane 0 highest): symmetric lanes would reach their host entropy-coding
     // phases together and leave the GPU idle; with priorities they drift apart and each lane's host
     // coding overlaps the lower-priority lanes' kernels.  MLIC_LANE_PRIORITY=0 disables.
-    int least = 0, greatest = 0;
-    HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     const char* e = std::getenv("MLIC_LANE_PRIORITY");
     const bool stagger = !(e && std::atoi(e) == 0);
-    const int idx = (int)lanes_.size();
-    const int prio = stagger ? std::min(least, greatest + idx) : least;
-    HIP_OK(hipStreamCreateWithPriority(&l->st, hipStreamNonBlocking, prio));
+    if (stagger) {
+      int least = 0, greatest = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      const int prio = std::min(least, greatest + (int)lanes_.size());
+      HIP_OK(hipStreamCreateWithPriority(&l->st, hipStreamNonBlocking, prio));
+    } else {
+      HIP_OK(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
+    }
     l->own_stream = true;
     l->prof = prof_;
     lanes_.push_back(std::move(l));

@@ -101,7 +101,9 @@ def test_smallcin(stride):
     (1, 96, 64, 9, 13, 3, 1, 0),                   # K-steps 27: odd count, tiny grid
     (2, 320, 256, 40, 120, 1, 1, GELU),            # (MLIC_V2_WIDE=1: 8-wave 256x256 tile)
     (2, 608, 224, 37, 120, 1, 1, RES),             # partial Cout and pixel tiles
-    (2, 192, 320, 40, 121, 3, 1, 0),               # 3x3, two 256-row Cout tiles
+    (2, 192, 320, 40, 121, 3, 1, 0),               # 3x3: 256-row tile + 64-row remainder launch
+    (2, 640, 320, 40, 120, 1, 1, GELU | RES),      # EP 640 -> 320: split launch with residual
+    (2, 192, 384, 24, 64, 3, 1, SHUFFLE),          # split launch under PixelShuffle (rows 256..383)
     (1, 32, 48, 8, 8, 1, 1, 0),                    # a single K-step
 ])
 def test_generic_tiles(impl, shape):
