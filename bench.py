@@ -153,7 +153,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     hs = [C.c_double() for _ in range(3)]
-    _lib.call("mlic_host_stats", net._handle, *[C.byref(v) for v in hs], 1)
+    _lib.call("mlic_host_stats", net._ensure_handle(dev), *[C.byref(v) for v in hs], 1)
     split["compress"] = split["decompress"] = 0.0
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -253,7 +253,7 @@ def main():
         with open(a.traffic_json) as f:
             tj = json.load(f)
         if (tj.get("model") == a.model and tj.get("H") == H and tj.get("W") == W
-                and tj.get("kernel", "") and tj["kernel"] in dom):
+                and tj.get("family", "") and tj["family"].replace(" ", "") in dom.replace(" ", "")):
             traffic = tj.get("conv_hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass

@@ -30,6 +30,12 @@ static int guard(F&& f) {
   return 1;
 }
 
+// Every entry point that takes a handle goes through here: a null handle is an error, not a crash.
+static Model& impl(mlic_model* m) {
+  MLIC_CHECK(m != nullptr && m->impl != nullptr, "null mlic_model handle");
+  return *m->impl;
+}
+
 static CdfTables make_tables(const int32_t* cdf, const int32_t* len, const int32_t* off, int n, int stride) {
   CdfTables t;
   t.n = n;
@@ -77,7 +83,7 @@ int mlic_forward(mlic_model* m, void* stream, const float* x, int B, int H, int 
                  float* z_lik, float vbr_scale) {
   return guard([&] {
     MLIC_CHECK(m && x && B > 0, "bad arguments");
-    m->impl->forward(x, B, H, W, x_hat, y_lik, z_lik, vbr_scale, (hipStream_t)stream);
+    impl(m).forward(x, B, H, W, x_hat, y_lik, z_lik, vbr_scale, (hipStream_t)stream);
   });
 }
 
@@ -86,7 +92,7 @@ int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t*
                             const int32_t* eb_off, int eb_n, int eb_stride) {
   return guard([&] {
     MLIC_CHECK(m, "null model");
-    m->impl->set_tables(make_tables(gc_cdf, gc_len, gc_off, gc_n, gc_stride),
+    impl(m).set_tables(make_tables(gc_cdf, gc_len, gc_off, gc_n, gc_stride),
                         make_tables(eb_cdf, eb_len, eb_off, eb_n, eb_stride));
   });
 }
@@ -94,13 +100,13 @@ int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t*
 int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale) {
   return guard([&] {
     MLIC_CHECK(m && x && B > 0, "bad arguments");
-    m->impl->compress(x, B, H, W, vbr_scale, (hipStream_t)stream);
+    impl(m).compress(x, B, H, W, vbr_scale, (hipStream_t)stream);
   });
 }
 
 int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len) {
   return guard([&] {
-    const EncodedImage& e = m->impl->encoded(b);
+    const EncodedImage& e = impl(m).encoded(b);
     *y_len = e.y.size();
     *z_len = e.z.size();
   });
@@ -108,7 +114,7 @@ int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len) {
 
 int mlic_encoded_copy(mlic_model* m, int b, uint8_t* y, uint8_t* z) {
   return guard([&] {
-    const EncodedImage& e = m->impl->encoded(b);
+    const EncodedImage& e = impl(m).encoded(b);
     std::memcpy(y, e.y.data(), e.y.size());
     std::memcpy(z, e.z.data(), e.z.size());
   });
@@ -117,7 +123,7 @@ int mlic_encoded_copy(mlic_model* m, int b, uint8_t* y, uint8_t* z) {
 int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32_t* y_sym, int32_t* y_idx,
                          int32_t* z_sym) {
   return guard([&] {
-    const EncodedImage& e = m->impl->encoded(b);
+    const EncodedImage& e = impl(m).encoded(b);
     *n_y = (int64_t)e.y_sym.size();
     *n_z = (int64_t)e.z_sym.size();
     if (y_sym) std::memcpy(y_sym, e.y_sym.data(), e.y_sym.size() * 4);
@@ -131,41 +137,41 @@ int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const 
                     float vbr_scale) {
   return guard([&] {
     MLIC_CHECK(m && y && z && x_hat && B > 0 && hz > 0 && wz > 0, "bad arguments");
-    m->impl->decompress(y, y_len, z, z_len, B, hz, wz, x_hat, vbr_scale, (hipStream_t)stream);
+    impl(m).decompress(y, y_len, z, z_len, B, hz, wz, x_hat, vbr_scale, (hipStream_t)stream);
   });
 }
 
 int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, const float* in0, const float* in1,
                     int B, int Cin, int H, int W, float* out) {
-  return guard([&] { m->impl->run_module(which, idx, in0, in1, B, Cin, H, W, out, (hipStream_t)stream); });
+  return guard([&] { impl(m).run_module(which, idx, in0, in1, B, Cin, H, W, out, (hipStream_t)stream); });
 }
 
 int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights) {
   return guard([&] {
-    *arena = m->impl->arena_bytes();
-    *weights = m->impl->weight_bytes();
+    *arena = impl(m).arena_bytes();
+    *weights = impl(m).weight_bytes();
   });
 }
 
 int mlic_set_precision(mlic_model* m, int precision) {
   return guard([&] {
     MLIC_CHECK(precision >= PREC_F32 && precision <= PREC_F16X3_V2, "precision must be 0 (f32), 1 or 2 (f16x3)");
-    m->impl->set_precision(precision);
+    impl(m).set_precision(precision);
   });
 }
 
 int mlic_set_lanes(mlic_model* m, int lanes) {
-  return guard([&] { m->impl->set_lanes(lanes); });
+  return guard([&] { impl(m).set_lanes(lanes); });
 }
 
 int mlic_set_profiling(mlic_model* m, int on) {
-  return guard([&] { m->impl->set_profiling(on != 0); });
+  return guard([&] { impl(m).set_profiling(on != 0); });
 }
 
 int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, double* flops, double* bytes) {
   return guard([&] {
     MLIC_CHECK(cat >= 0 && cat < PCAT_COUNT, "profile category");
-    ProfStat s = m->impl->profile_read(cat);
+    ProfStat s = impl(m).profile_read(cat);
     *launches = s.launches;
     *ms = s.ms;
     *flops = s.flops;
@@ -175,7 +181,7 @@ int mlic_profile_read(mlic_model* m, int cat, int64_t* launches, double* ms, dou
 
 int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written) {
   return guard([&] {
-    std::string s = m->impl->profile_layers();
+    std::string s = impl(m).profile_layers();
     *written = s.size();
     if (buf && cap) {
       const size_t n = std::min(cap - 1, s.size());
@@ -246,7 +252,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
 
 int mlic_host_stats(mlic_model* m, double* enc_ms, double* dec_ms, double* wait_ms, int reset) {
   return guard([&] {
-    HostStats& h = m->impl->host_stats();
+    HostStats& h = impl(m).host_stats();
     *enc_ms = h.enc_ns.load() * 1e-6;
     *dec_ms = h.dec_ns.load() * 1e-6;
     *wait_ms = h.wait_ns.load() * 1e-6;

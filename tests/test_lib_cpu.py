@@ -23,6 +23,15 @@ def test_library_exports_every_declared_symbol():
     assert lib.mlic_version().startswith(b"mlic_hip")
 
 
+def test_null_handle_is_an_error_not_a_crash():
+    import ctypes as C
+    hs = [C.c_double() for _ in range(3)]
+    with pytest.raises(_lib.MlicError, match="null mlic_model handle"):
+        _lib.call("mlic_host_stats", None, *[C.byref(v) for v in hs], 1)
+    with pytest.raises(_lib.MlicError, match="null mlic_model handle"):
+        _lib.call("mlic_set_lanes", None, 2)
+
+
 def test_gaussian_tables_match_reference_update(golden):
     g = golden("scale_table.npz")
     cdf, length, offset, table = entropy.gaussian_tables(entropy.get_scale_table())
