@@ -35,6 +35,8 @@ sys.path.insert(0, ROOT)
 def kernel_peak(name: str):
     if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv_halo")):
         return 2500.0 / 3, "3 x v_mfma_f32_32x32x16_f16 per fp32 product (split-fp16)"
+    if name.startswith("conv_x4"):
+        return 2500.0 / 3, "3 x v_mfma_f32_16x16x32_f16 per fp32 product (split-fp16, LDS-DMA staged)"
     if name.startswith("conv_mfma"):
         return 157.3, "v_mfma_f32_32x32x2_f32"
     return 157.3, "fp32 VALU FMA"

@@ -228,9 +228,18 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     P.out_bs = (int64_t)Cout * Ho * Wo;
     P.out_cs = (int64_t)Ho * Wo;
     P.epi = shuffle ? EPI_SHUFFLE : 0;
-    const ConvWeights cw{wp, wh, wl, cin_pad};
+    _Float16* wx = nullptr;
+    if (conv_x4_ok(P, cin_pad)) {
+      HIP_OK(hipMalloc((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2));
+      x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, nullptr);
+    }
+    const ConvWeights cw{wp, wh, wl, cin_pad, wx};
     const int which = impl == 3 ? conv_select(P, cw, 2) : impl;  // 3 = what the model runs (precision 2)
-    auto launch = [&] { conv_run(which, P, cw, nullptr); };
+    if (which == CONV_X4) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
+    void* ws = nullptr;
+    const int64_t wsb = conv_ws_bytes(which, P, cw);
+    if (wsb > 0) HIP_OK(hipMalloc(&ws, wsb));
+    auto launch = [&] { conv_run(which, P, cw, nullptr, ws); };
     launch();
     HIP_OK(hipDeviceSynchronize());
     hipEvent_t a, b;
@@ -246,7 +255,8 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     *tflops = 2.0 * (double)B * Cout * Ho * Wo * Cin * K * K / (*ms_per * 1e-3) / 1e12;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl}) (void)hipFree(p);
+    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl, (void*)wx, ws})
+      if (p) (void)hipFree(p);
   });
 }
 
@@ -305,13 +315,24 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     MLIC_CHECK(!(epi & EPI_RES) || res, "residual epilogue needs res");
     P.aux = aux; P.aux_bs = (int64_t)Cout * Ho * Wo;
     P.res = res; P.res_bs = P.out_bs;
-    const ConvWeights cw{wp, wh, wl, cin_pad};
+    _Float16* wx = nullptr;
+    if (conv_x4_ok(P, cin_pad)) {
+      HIP_OK(hipMallocAsync((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2, st));
+      x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, st);
+    }
+    const ConvWeights cw{wp, wh, wl, cin_pad, wx};
     const int which = impl < 0 ? conv_select(P, cw, 2) : impl;
     if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
     if (which == CONV_NARROW) MLIC_CHECK(conv_narrow_ok(P), "narrow: unsupported shape");
     if (which == CONV_SMALLCIN) MLIC_CHECK(conv_smallcin_ok(P), "smallcin: unsupported shape");
     if (which == CONV_HALO) MLIC_CHECK(conv_halo_ok(P, cin_pad), "halo: unsupported shape");
-    conv_run(which, P, cw, st);
+    if (which == CONV_X4) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
+    void* ws = nullptr;
+    const int64_t wsb = conv_ws_bytes(which, P, cw);
+    if (wsb > 0) HIP_OK(hipMallocAsync(&ws, wsb, st));
+    conv_run(which, P, cw, st, ws);
+    if (ws) HIP_OK(hipFreeAsync(ws, st));
+    if (wx) HIP_OK(hipFreeAsync(wx, st));
     HIP_OK(hipFreeAsync(wp, st));
     HIP_OK(hipFreeAsync(wh, st));
     HIP_OK(hipFreeAsync(wl, st));

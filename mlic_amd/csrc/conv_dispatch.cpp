@@ -2,7 +2,18 @@
 // the per-kernel C-ABI test entry (mlic_conv_run) and the micro-benchmark all run the same choice.
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace mlic {
+
+// $MLIC_X4=0 disables the LDS-DMA x4 kernel (A/B switch)
+static bool x4_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_X4");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (conv_smallcin_ok(P)) return CONV_SMALLCIN;  // exact fp32 VALU, all precisions
@@ -11,6 +22,10 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (precision == 1) return CONV_X3;
   // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
   if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
+  // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs) once the grid fills the chip
+  if (w.wx4 && x4_on() && P.K == 3 && P.Cout >= 192 && conv_x4_ok(P, w.cin_pad) &&
+      (int64_t)((P.Cout + 255) / 256) * ((P.W + 31) / 32) * ((P.H + 7) / 8) * P.B >= 256)
+    return CONV_X4;
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay
   if (P.K == 5 && conv_halo_ok(P, w.cin_pad) &&
@@ -30,11 +45,16 @@ int conv_prof_cat(int impl, const ConvParams& P) {
     case CONV_PW: return PCAT_CONV_PW;
     case CONV_NARROW: return PCAT_CONV_NARROW;
     case CONV_HALO: return PCAT_CONV_HALO;
+    case CONV_X4: return PCAT_CONV_X4;
     default: return PCAT_CONV_SMALLCIN;
   }
 }
 
-void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t st) {
+int64_t conv_ws_bytes(int impl, const ConvParams& P, const ConvWeights& w) {
+  return impl == CONV_X4 ? 2 * x4_act_halves(P, w.cin_pad) : 0;
+}
+
+void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t st, void* ws) {
   switch (impl) {
     case CONV_F32: conv_forward(P, st); break;
     case CONV_X3: conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, st); break;
@@ -43,6 +63,13 @@ void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t s
     case CONV_NARROW: conv_narrow_forward(P, st); break;
     case CONV_SMALLCIN: conv_smallcin_forward(P, st); break;
     case CONV_HALO: conv_halo_forward(P, w.wh, w.wl, w.cin_pad, st); break;
+    case CONV_X4: {
+      MLIC_CHECK(ws && w.wx4, "conv_x4: workspace and packed weights required");
+      _Float16* act = static_cast<_Float16*>(ws);
+      x4_pack_act(P, w.cin_pad, act, st);
+      conv_x4_forward(P, act, w.wx4, w.cin_pad, st);
+      break;
+    }
     default: throw Error("mlic: unknown conv implementation " + std::to_string(impl));
   }
 }
@@ -56,7 +83,8 @@ const char* prof_cat_name(int cat) {
       "pw_resident_kernel",
       "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "conv_halo_kernel",
       "dw3x3_kernel",
-      "local_attn_kernel",           "linear_attention",          "elementwise"};
+      "local_attn_kernel",           "linear_attention",          "elementwise",
+      "conv_x4_kernel"};
   return (cat >= 0 && cat < PCAT_COUNT) ? names[cat] : "";
 }
 

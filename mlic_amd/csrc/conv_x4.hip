@@ -1,0 +1,295 @@
+// Split-fp16 implicit-GEMM convolution with both operands staged by LDS-DMA (gfx950), "x4".
+//
+// Same arithmetic as conv_f16x3.hip (v = hi + lo + r, a.b = lo_a.hi_b + hi_a.lo_b + hi_a.hi_b on the
+// fp16 MFMA pipe with fp32 accumulation), re-organised so the K loop is a pure DMA -> LDS -> MFMA
+// pipeline with no register staging:
+//   * activations are first packed by x4_pack_act_kernel into a zero-bordered, channel-chunked
+//     split layout  act[b][chunk][Hp][Wp][64 halves]  (hi of 32 channels | lo of the same 32),
+//     Hp = H + 2 pad, Wp = W + 2 pad.  One 128-byte line = one pixel's 32-channel chunk, so the B
+//     tile of a (tap, chunk) K-step is 256 whole lines gathered straight into LDS with
+//     global_load_lds_dwordx4 (the border is real zeros: no bounds checks in the loop);
+//   * weights are packed once into the exact LDS image of each K-step, [ct][step][BM][64 halves];
+//   * LDS rows are 128 bytes; 16-byte granule G of row n sits at G ^ ((n >> 1) & 7), applied on the
+//     global SOURCE address of the DMA (the LDS destination of a glds is lane-linear) and on the
+//     read, which makes every ds_read_b128 fragment read of v_mfma_f32_16x16x32_f16 conflict-free;
+//   * two LDS stages: while step s computes, step s+1's DMA is in flight; one barrier per step.
+// Block tile: BM (Cout) x 256 pixels (8 rows x 32 columns), 8 waves, wave tile 64 x (256 / waves_n).
+// K-step = one 32-channel chunk at one tap (chunk-major, tap-minor, so consecutive steps re-read
+// the same input lines shifted by a pixel: L2 hits).
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace mlic {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+namespace {
+constexpr int X4T = 512;               // threads (8 waves)
+constexpr int TR = 8, TC = 32;         // pixel tile: 8 rows x 32 columns
+constexpr int BN = TR * TC;            // 256 pixels
+constexpr int ROWB = 128;              // LDS row: 32 hi + 32 lo halves
+constexpr int ROWH = 64;               // halves per row
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule) {
+  return *reinterpret_cast<const half8*>(base + row * ROWB + ((granule ^ swz(row)) << 4));
+}
+}  // namespace
+
+template <int K, int BM>
+__global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
+                                                      const _Float16* __restrict__ wx, int nchunk) {
+  constexpr int KK = K * K;
+  constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
+  constexpr int WN = BN / WAVES_N;        // pixels per wave
+  constexpr int TM = 4, TN = WN / 16;     // 16x16 fragments per wave
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int NA = A_BYTES / 1024 / 8;  // 1 KB glds instructions per wave for A
+  constexpr int NB = B_BYTES / 1024 / 8;  // ... for B
+  static_assert(NA >= 1 && NB == 4 && 2 * STAGE <= 160 * 1024, "x4 tile");
+  __shared__ __attribute__((aligned(1024))) char sm[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int H = P.H, W = P.W, pad = K / 2;
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const int ntx = (W + TC - 1) / TC;
+  const int nct = gridDim.x, npt = gridDim.y, nblk = nct * npt;
+  const int bid = blockIdx.y * nct + blockIdx.x;
+  int logical = bid;
+  if (nblk >= 16) {  // XCD-aware bijective remap (the blocks of one XCD take consecutive tiles)
+    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int ct = logical % nct, pt = logical / nct;
+  const int oy0 = (pt / ntx) * TR, ox0 = (pt % ntx) * TC;
+  const int b = blockIdx.z;
+  const int nsteps = nchunk * KK;
+
+  // per-lane DMA sources.  B: instruction i of this wave moves pixels n = (wave*NB + i)*8 + lane/8,
+  // physical granule lane%8 <- logical granule (lane%8) ^ swz(n).  Pixels past the image edge read a
+  // clamped (valid) line; their outputs are discarded.
+  const int64_t plane = (int64_t)Hp * Wp * ROWH;  // halves per (image, chunk)
+  const _Float16* bsrc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = (wave * NB + i) * 8 + (lane >> 3);
+    const int oy = min(oy0 + n / TC, H - 1), ox = min(ox0 + n % TC, W - 1);
+    const int G = (lane & 7) ^ swz(n);
+    bsrc[i] = act + (int64_t)b * nchunk * plane + ((int64_t)oy * Wp + ox) * ROWH + G * 8;
+  }
+  const _Float16* asrc = wx + ((int64_t)ct * nsteps * BM) * ROWH + (wave * NA) * 512 + lane * 8;
+
+  auto issue = [&](int s, int buf) {
+    char* st = sm + buf * STAGE;
+    const _Float16* a = asrc + (int64_t)s * BM * ROWH;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) glds16(a + i * 512, st + (wave * NA + i) * 1024);
+    const int cc = s / KK, tap = s - cc * KK;
+    const int ky = tap / K, kx = tap - ky * K;
+    const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) glds16(bsrc[i] + d, st + A_BYTES + (wave * NB + i) * 1024);
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int G = lane >> 4, l16 = lane & 15;
+  issue(0, 0);
+  for (int s = 0; s < nsteps; ++s) {
+    // step s's DMA (issued by every wave) has landed; every wave is done reading the other buffer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+    const char* As = sm + (s & 1) * STAGE;
+    const char* Bs = As + A_BYTES;
+    half8 ah[TM], al[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * 64 + i * 16 + l16;
+      ah[i] = lds_frag(As, row, G);
+      al[i] = lds_frag(As, row, G + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wn * WN + j * 16 + l16;
+      const half8 bh = lds_frag(Bs, n, G);
+      const half8 bl = lds_frag(Bs, n, G + 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue through a wave-private LDS strip (the stage buffers are free once every wave is past
+  // its last read): C/D map of 16x16x32 is (row 4*(lane>>4) + e, col lane&15) with row = Cout and
+  // col = pixel; per 16-row group the wave transposes to rows of WN pixels and stores each Cout row
+  // as 128-byte runs.  Every acc index stays compile-time (a runtime-indexed acc goes to scratch).
+  constexpr int EP = WN + 4;  // row pitch (floats): the 4 row groups of a write land on distinct banks
+  __syncthreads();
+  float* ep = reinterpret_cast<float*>(sm) + wave * 16 * EP;
+  const int co_w = ct * BM + wm * 64;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ep[(4 * G + e) * EP + j * 16 + l16] = acc[i][j][e];
+#pragma unroll 1
+    for (int k = 0; k < 16 * WN / 64; ++k) {
+      const int idx = k * 64 + lane;
+      const int r = idx / WN, n = idx % WN;
+      const int nn = wn * WN + n;
+      const int oy = oy0 + nn / TC, ox = ox0 + nn % TC;
+      const int co = co_w + i * 16 + r;
+      const float v = ep[r * EP + n];
+      if (oy < H && ox < W && co < P.Cout) conv_store(P, b, co, oy * W + ox, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// activation packing: NCHW fp32 (multi-segment concat) -> act[b][chunk][Hp][Wp][hi 32 | lo 32]
+struct X4Pack {
+  Seg seg[MAXSEG];
+  int nseg, Cin, H, W, pad, nchunk, square;
+  _Float16* dst;
+};
+
+// grid (ceil(Hp*Wp / 64), nchunk, B), 256 threads: lane = position (64 consecutive), wave = 8-channel group
+__global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
+  const int Hp = Q.H + 2 * Q.pad, Wp = Q.W + 2 * Q.pad;
+  const int pos = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int cc = blockIdx.y, b = blockIdx.z;
+  if (pos >= Hp * Wp) return;
+  const int y = pos / Wp - Q.pad, x = pos % Wp - Q.pad;
+  const bool inb = y >= 0 && y < Q.H && x >= 0 && x < Q.W;
+  const int ch0 = cc * 32 + 8 * g;
+  int s = 0, c0 = 0;  // 8-channel groups never straddle a segment (segments are 16-aligned)
+  while (s + 1 < Q.nseg && ch0 >= c0 + Q.seg[s].C) { c0 += Q.seg[s].C; ++s; }
+  const Seg sg = Q.seg[s];
+  const int64_t HW = (int64_t)Q.H * Q.W;
+  const float* src = sg.p + (int64_t)b * sg.bs + (int64_t)(ch0 - c0) * HW + (int64_t)y * Q.W + x;
+  half8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool ok = inb && ch0 + j < Q.Cin && ch0 - c0 + j < sg.C;
+    float v = ok ? src[(int64_t)j * HW] : 0.0f;
+    if (Q.square) v *= v;
+    const _Float16 hv = (_Float16)v;
+    h[j] = hv;
+    l[j] = (_Float16)(v - (float)hv);
+  }
+  _Float16* d = Q.dst + (((int64_t)b * Q.nchunk + cc) * Hp * Wp + pos) * ROWH + 8 * g;
+  *reinterpret_cast<half8*>(d) = h;
+  *reinterpret_cast<half8*>(d + 32) = l;
+}
+
+// weights: hi/lo [Cout][KK][cin_pad] -> [ct][step = chunk*KK + tap][BM rows][64 halves], swizzled
+__global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _Float16* __restrict__ wl,
+                                       _Float16* __restrict__ dst, int Cout, int KK, int cin_pad, int BM,
+                                       int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int e = (int)(i % ROWH);           // physical half within the row
+  const int row = (int)((i / ROWH) % BM);
+  const int64_t ts = i / ((int64_t)ROWH * BM);  // ct * nsteps + step
+  const int nchunk = cin_pad / 32, nsteps = nchunk * KK;
+  const int step = (int)(ts % nsteps), ct = (int)(ts / nsteps);
+  const int cc = step / KK, tap = step - cc * KK;
+  const int Gp = e >> 3, G = Gp ^ ((row >> 1) & 7);  // logical granule stored at physical Gp
+  const int k = (G & 3) * 8 + (e & 7);               // channel within the chunk
+  const int co = ct * BM + row;
+  _Float16 v = (_Float16)0.0f;
+  if (co < Cout) {
+    const int64_t off = ((int64_t)co * KK + tap) * cin_pad + cc * 32 + k;
+    v = G < 4 ? wh[off] : wl[off];
+  }
+  dst[i] = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+int x4_bm(int Cout) { return Cout >= 192 ? 256 : 128; }
+
+int64_t x4_weight_halves(int Cout, int KK, int cin_pad) {
+  const int bm = x4_bm(Cout);
+  return (int64_t)((Cout + bm - 1) / bm) * bm * KK * (cin_pad / 32) * ROWH;
+}
+
+void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, int cin_pad, _Float16* dst,
+                     hipStream_t st) {
+  const int64_t n = x4_weight_halves(Cout, KK, cin_pad);
+  hipLaunchKernelGGL(x4_pack_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wh, wl, dst, Cout,
+                     KK, cin_pad, x4_bm(Cout), n);
+  HIP_OK(hipGetLastError());
+}
+
+int64_t x4_act_halves(const ConvParams& P, int cin_pad) {
+  const int pad = P.K / 2;
+  return (int64_t)P.B * (cin_pad / 32) * (P.H + 2 * pad) * (P.W + 2 * pad) * ROWH;
+}
+
+bool conv_x4_ok(const ConvParams& P, int cin_pad) {
+  if (!(P.K == 1 || P.K == 3 || P.K == 5) || P.stride != 1 || P.pad != P.K / 2) return false;
+  if (P.Ho != P.H || P.Wo != P.W || cin_pad % 32 != 0 || cin_pad < P.Cin || P.Cout < 64) return false;
+  for (int s = 0; s + 1 < P.nseg; ++s)
+    if (P.seg[s].C % 16 != 0) return false;
+  return true;
+}
+
+void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st) {
+  X4Pack Q{};
+  for (int s = 0; s < P.nseg; ++s) Q.seg[s] = P.seg[s];
+  Q.nseg = P.nseg;
+  Q.Cin = P.Cin;
+  Q.H = P.H;
+  Q.W = P.W;
+  Q.pad = P.K / 2;
+  Q.nchunk = cin_pad / 32;
+  Q.square = (P.epi & EPI_SQUARE_IN) ? 1 : 0;
+  Q.dst = dst;
+  const int npos = (P.H + 2 * Q.pad) * (P.W + 2 * Q.pad);
+  hipLaunchKernelGGL(x4_pack_act_kernel, dim3((npos + 63) / 64, Q.nchunk, P.B), dim3(256), 0, st, Q);
+  HIP_OK(hipGetLastError());
+}
+
+template <int K, int BM>
+static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st) {
+  const int ntx = (P.W + TC - 1) / TC, nty = (P.H + TR - 1) / TR;
+  dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B);
+  hipLaunchKernelGGL((conv_x4_kernel<K, BM>), grid, dim3(X4T), 0, st, P, act, wx, nchunk);
+  HIP_OK(hipGetLastError());
+}
+
+void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st) {
+  MLIC_CHECK(conv_x4_ok(P, cin_pad) && act && wx, "conv_x4: unsupported shape");
+  // the ConvParams input segments are not read: the packed copy (x4_pack_act) is
+  ConvParams Q = P;
+  Q.epi &= ~EPI_SQUARE_IN;
+  const int nchunk = cin_pad / 32;
+  const bool wide = x4_bm(P.Cout) == 256;
+  switch (P.K) {
+    case 1: wide ? launch_x4<1, 256>(Q, act, wx, nchunk, st) : launch_x4<1, 128>(Q, act, wx, nchunk, st); break;
+    case 3: wide ? launch_x4<3, 256>(Q, act, wx, nchunk, st) : launch_x4<3, 128>(Q, act, wx, nchunk, st); break;
+    default: wide ? launch_x4<5, 256>(Q, act, wx, nchunk, st) : launch_x4<5, 128>(Q, act, wx, nchunk, st); break;
+  }
+}
+
+}  // namespace mlic

@@ -30,18 +30,33 @@ void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
 bool conv_smallcin_ok(const ConvParams& P);
 void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 
+// LDS-DMA split-fp16 conv (conv_x4.hip): activations packed per call into a zero-bordered split
+// layout (x4_pack_act, workspace of x4_act_halves halves), weights packed once (x4_pack_weights)
+int x4_bm(int Cout);
+int64_t x4_weight_halves(int Cout, int KK, int cin_pad);
+void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, int cin_pad, _Float16* dst,
+                     hipStream_t st);
+int64_t x4_act_halves(const ConvParams& P, int cin_pad);
+bool conv_x4_ok(const ConvParams& P, int cin_pad);
+void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st);
+void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st);
+
 // kernel-family selection (conv_dispatch.cpp)
 enum ConvImpl : int {
-  CONV_F32 = 0, CONV_X3 = 1, CONV_X3V2 = 2, CONV_PW = 3, CONV_NARROW = 4, CONV_SMALLCIN = 5, CONV_HALO = 6
+  CONV_F32 = 0, CONV_X3 = 1, CONV_X3V2 = 2, CONV_PW = 3, CONV_NARROW = 4, CONV_SMALLCIN = 5, CONV_HALO = 6,
+  CONV_X4 = 7
 };
 struct ConvWeights {
   const float* wpk;  // fp32 packed [K*K][Cin][Cout] (in ConvParams too)
   const _Float16* wh;
   const _Float16* wl;
   int cin_pad;
+  const _Float16* wx4 = nullptr;  // x4_pack_weights image (null: CONV_X4 not available)
 };
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision);
-void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t st);
+// device workspace conv_run needs for impl (bytes; 0 = none)
+int64_t conv_ws_bytes(int impl, const ConvParams& P, const ConvWeights& w);
+void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t st, void* ws = nullptr);
 
 // live-profiling categories (one per kernel family / tile instantiation)
 enum ProfCat : int {
@@ -57,7 +72,8 @@ enum ProfCat : int {
   PCAT_LOCAL = 17,
   PCAT_LINATT = 18,
   PCAT_ELEM = 19,
-  PCAT_COUNT = 20
+  PCAT_CONV_X4 = 20,
+  PCAT_COUNT = 21
 };
 int conv_prof_cat(int impl, const ConvParams& P);
 const char* prof_cat_name(int cat);

@@ -172,6 +172,29 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     convs_[p + ".__gdn"] = w;
   }
   MLIC_CHECK(off <= total, "weight block overflow");
+  // LDS-image copies for the x4 kernel: the stride-1 KxK convs it can serve (K in 1, 3, 5)
+  {
+    int64_t nx = 0;
+    for (auto& kv : convs_) {
+      const ConvW& w = kv.second;
+      if (w.wh && (w.K == 1 || w.K == 3 || w.K == 5) && w.Cout >= 64)
+        nx += (x4_weight_halves(w.Cout, w.K * w.K, w.cin_pad) + 127) & ~(int64_t)127;
+    }
+    if (nx > 0) {
+      _Float16* xb = nullptr;
+      HIP_OK(hipMalloc(&xb, nx * sizeof(_Float16)));
+      owned_.push_back(xb);
+      wbytes_ += nx * sizeof(_Float16);
+      int64_t xo = 0;
+      for (auto& kv : convs_) {
+        ConvW& w = kv.second;
+        if (!(w.wh && (w.K == 1 || w.K == 3 || w.K == 5) && w.Cout >= 64)) continue;
+        w.wx4 = xb + xo;
+        x4_pack_weights(w.wh, w.wl, w.Cout, w.K * w.K, w.cin_pad, w.wx4, st);
+        xo += (x4_weight_halves(w.Cout, w.K * w.K, w.cin_pad) + 127) & ~(int64_t)127;
+      }
+    }
+  }
   // relative position index (attention.py:28-39), int32
   {
     const int win = cfg_.win, ww = win * win;
@@ -314,9 +337,13 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
   const double outn = (double)L().B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * cin * w.K * w.K;
   const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad};
+  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4};
   const int impl = conv_select(P, cw, precision_);
-  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st); }, w.name);
+  const int64_t wsb = conv_ws_bytes(impl, P, cw);
+  const size_t m = L().arena.mark();
+  void* ws = wsb > 0 ? static_cast<void*>(L().arena.alloc((wsb + 3) / 4)) : nullptr;
+  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st, ws); }, w.name);
+  L().arena.release(m);  // stream-ordered: the next user of this memory runs after the conv
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {

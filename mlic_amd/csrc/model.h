@@ -31,6 +31,7 @@ struct ConvW {
   _Float16* wh = nullptr;    // split hi/lo [Cout][K*K][cin_pad]  (f16x3 MFMA path)
   _Float16* wl = nullptr;
   int cin_pad = 0;
+  _Float16* wx4 = nullptr;   // x4 LDS-image weights [ct][step][BM][64]     (conv_x4 path)
   std::string name;          // state_dict prefix (profiling)
 };
 

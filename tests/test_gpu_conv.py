@@ -11,7 +11,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 GELU, GDN, IGDN, RES, SHUFFLE, SQUARE = 1, 2, 4, 64, 128, 256
-F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, AUTO = 0, 1, 2, 3, 4, 5, 6, -1
+F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, X4, AUTO = 0, 1, 2, 3, 4, 5, 6, 7, -1
 
 
 def reference(x, w, b, stride, epi, res):
@@ -132,6 +132,29 @@ def test_halo(shape):
 def test_halo_k1_k5(shape):
     B, cin, cout, H, W, K, epi = shape
     check(*run(HALO, B, cin, cout, H, W, K, epi=epi))
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 192, 768, 24, 64, 3, SHUFFLE | GELU),   # g_s subpel conv: 3 x 256-row Cout tiles, 2 x 3 pixel tiles
+    (1, 192, 768, 19, 45, 3, SHUFFLE),          # ragged pixel tiles at every edge
+    (2, 320, 256, 17, 30, 3, GELU | RES),       # 10 chunks, residual
+    (1, 100, 200, 9, 33, 3, 0),                 # Cin not a multiple of 32, Cout 200 (partial 256 tile)
+    (2, 128, 128, 16, 40, 3, GDN | SQUARE),     # 128-row tile (Cout < 192), GDN epilogue on the packed x^2
+    (2, 960, 320, 17, 30, 1, GELU),             # 1x1 GEMM (entropy parameters), partial second tile
+    (1, 288, 96, 13, 37, 5, 0),                 # 5x5 reprojection, 128-row tile
+    (1, 480, 1920, 8, 16, 3, SHUFFLE | GELU),   # h_s subpel 480 -> 1920, 8 Cout tiles
+])
+def test_x4(shape):
+    B, cin, cout, H, W, K, epi = shape
+    check(*run(X4, B, cin, cout, H, W, K, epi=epi))
+
+
+def test_x4_auto_selection():
+    """A g_s-shaped subpel conv whose grid fills the chip runs on x4 under automatic selection."""
+    y, ref = run(AUTO, 2, 192, 768, 128, 192, 3, epi=SHUFFLE | GELU)
+    check(y, ref)
+    y2, _ = run(X4, 2, 192, 768, 128, 192, 3, epi=SHUFFLE | GELU)
+    assert torch.equal(y, y2)
 
 
 def test_auto_matches_selected_family():
