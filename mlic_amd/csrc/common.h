@@ -126,4 +126,71 @@ __device__ __forceinline__ void conv_store(const ConvParams& P, int b, int co, i
   P.out[(int64_t)b * P.out_bs + off] = v;
 }
 
+// vectorised forms of conv_store for kernels that stage their output tile (conv_x4): four outputs
+// per lane as one 16-byte store.  conv_store4: channel co at pixels p .. p+3 of one row (no pixel
+// shuffle).  conv_store_shuf4: under PixelShuffle(2), channels co0 (= 4 oc + 2 dy) and co0 + 1 at
+// pixels p, p+1 fill x2 = 2 ow .. 2 ow + 3 of output row 2 oh + dy; v = (co0@p, co0+1@p, co0@p+1,
+// co0+1@p+1).  Callers check 16-byte alignment of every operand (conv_vec_ok) and full validity.
+__device__ __forceinline__ bool conv_vec_ok(const ConvParams& P) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(P.out) | reinterpret_cast<uintptr_t>(P.aux) |
+                      reinterpret_cast<uintptr_t>(P.res);
+  return (a & 15) == 0 && ((P.out_bs | P.out_cs | P.aux_bs | P.res_bs) & 3) == 0 && (P.Wo & 3) == 0;
+}
+
+__device__ __forceinline__ void conv_store4(const ConvParams& P, int b, int co, int p, float4 v) {
+  const int epi = P.epi;
+  float a[4] = {v.x, v.y, v.z, v.w};
+  const float bi = P.bias ? P.bias[co] : 0.0f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] += bi;
+    if (epi & EPI_GELU) a[e] = gelu_erf(a[e]);
+  }
+  if (epi & (EPI_GDN | EPI_IGDN)) {
+    const float4 x = *reinterpret_cast<const float4*>(P.aux + (int64_t)b * P.aux_bs + (int64_t)co * P.Ho * P.Wo + p);
+    const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] = (epi & EPI_GDN) ? xs[e] * (1.0f / sqrtf(a[e])) : xs[e] * sqrtf(a[e]);
+  }
+  if (epi & EPI_TANH_HALF) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] = 0.5f * tanhf(a[e]);
+  }
+  if (epi & (EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR)) {
+    const int oh = p / P.Wo, ow = p - oh * P.Wo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool anc = is_anchor(oh, ow + e);
+      if ((epi & EPI_MASK_ANCHOR) && !anc) a[e] = 0.0f;
+      if ((epi & EPI_MASK_NONANCHOR) && anc) a[e] = 0.0f;
+    }
+  }
+  const int64_t off = (int64_t)co * P.out_cs + p;
+  if (epi & EPI_RES) {
+    const float4 r = *reinterpret_cast<const float4*>(P.res + (int64_t)b * P.res_bs + off);
+    a[0] = r.x + a[0]; a[1] = r.y + a[1]; a[2] = r.z + a[2]; a[3] = r.w + a[3];
+  }
+  *reinterpret_cast<float4*>(P.out + (int64_t)b * P.out_bs + off) = make_float4(a[0], a[1], a[2], a[3]);
+}
+
+// GDN / masks never combine with the pixel shuffle in this model (checked by the caller)
+__device__ __forceinline__ void conv_store_shuf4(const ConvParams& P, int b, int co0, int p, float4 v) {
+  const int epi = P.epi;
+  float a[4] = {v.x, v.y, v.z, v.w};
+  const float b0 = P.bias ? P.bias[co0] : 0.0f, b1 = P.bias ? P.bias[co0 + 1] : 0.0f;
+  a[0] += b0; a[1] += b1; a[2] += b0; a[3] += b1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (epi & EPI_GELU) a[e] = gelu_erf(a[e]);
+    if (epi & EPI_TANH_HALF) a[e] = 0.5f * tanhf(a[e]);
+  }
+  const int oh = p / P.Wo, ow = p - oh * P.Wo;
+  const int64_t off = (int64_t)(co0 >> 2) * P.out_cs + (int64_t)(2 * oh + ((co0 >> 1) & 1)) * (2 * P.Wo) + 2 * ow;
+  if (epi & EPI_RES) {
+    const float4 r = *reinterpret_cast<const float4*>(P.res + (int64_t)b * P.res_bs + off);
+    a[0] = r.x + a[0]; a[1] = r.y + a[1]; a[2] = r.z + a[2]; a[3] = r.w + a[3];
+  }
+  *reinterpret_cast<float4*>(P.out + (int64_t)b * P.out_bs + off) = make_float4(a[0], a[1], a[2], a[3]);
+}
+
 }  // namespace mlic

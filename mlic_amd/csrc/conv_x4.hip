@@ -12,7 +12,9 @@
 //   * LDS rows are 128 bytes; 16-byte granule G of row n sits at G ^ ((n >> 1) & 7), applied on the
 //     global SOURCE address of the DMA (the LDS destination of a glds is lane-linear) and on the
 //     read, which makes every ds_read_b128 fragment read of v_mfma_f32_16x16x32_f16 conflict-free;
-//   * two LDS stages: while step s computes, step s+1's DMA is in flight; one barrier per step.
+//   * a 2-deep A ring and a 3-deep B ring: while step s computes, the weights of step s+1 and the
+//     activations of steps s+1 and s+2 are in flight (counted vmcnt, raw s_barrier: a
+//     __syncthreads() would drain every DMA); one barrier per step.
 // Block tile: BM (Cout) x 256 pixels (8 rows x 32 columns), 8 waves, wave tile 64 x (256 / waves_n).
 // K-step = one 32-channel chunk at one tap (chunk-major, tap-minor, so consecutive steps re-read
 // the same input lines shifted by a pixel: L2 hits).
@@ -47,16 +49,17 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 
 template <int K, int BM>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
-                                                      const _Float16* __restrict__ wx, int nchunk) {
+                                                      const _Float16* __restrict__ wx, int nchunk, int abl) {
   constexpr int KK = K * K;
   constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WN = BN / WAVES_N;        // pixels per wave
   constexpr int TM = 4, TN = WN / 16;     // 16x16 fragments per wave
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
+  constexpr int B_OFF = 2 * A_BYTES, LDS = 2 * A_BYTES + 3 * B_BYTES;
   constexpr int NA = A_BYTES / 1024 / 8;  // 1 KB glds instructions per wave for A
   constexpr int NB = B_BYTES / 1024 / 8;  // ... for B
-  static_assert(NA >= 1 && NB == 4 && 2 * STAGE <= 160 * 1024, "x4 tile");
-  __shared__ __attribute__((aligned(1024))) char sm[2 * STAGE];
+  static_assert(NA >= 1 && NB == 4 && LDS <= 160 * 1024, "x4 tile");
+  __shared__ __attribute__((aligned(1024))) char sm[LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -89,16 +92,19 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   }
   const _Float16* asrc = wx + ((int64_t)ct * nsteps * BM) * ROWH + (wave * NA) * 512 + lane * 8;
 
-  auto issue = [&](int s, int buf) {
-    char* st = sm + buf * STAGE;
+  auto issue_a = [&](int s) {
+    char* st = sm + (s & 1) * A_BYTES;
     const _Float16* a = asrc + (int64_t)s * BM * ROWH;
 #pragma unroll
     for (int i = 0; i < NA; ++i) glds16(a + i * 512, st + (wave * NA + i) * 1024);
+  };
+  auto issue_b = [&](int s, int buf) {
+    char* st = sm + B_OFF + buf * B_BYTES;
     const int cc = s / KK, tap = s - cc * KK;
     const int ky = tap / K, kx = tap - ky * K;
     const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) glds16(bsrc[i] + d, st + A_BYTES + (wave * NB + i) * 1024);
+    for (int i = 0; i < NB; ++i) glds16(bsrc[i] + d, st + (wave * NB + i) * 1024);
   };
 
   floatx4 acc[TM][TN];
@@ -108,14 +114,24 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int G = lane >> 4, l16 = lane & 15;
-  issue(0, 0);
-  for (int s = 0; s < nsteps; ++s) {
-    // step s's DMA (issued by every wave) has landed; every wave is done reading the other buffer
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
-    const char* As = sm + (s & 1) * STAGE;
-    const char* Bs = As + A_BYTES;
+  // issue order: A0 B0 B1 | step 0: A1 B2 | step 1: A2 B3 | ...  At the top of step s the newest NB
+  // requests are B(s+1); everything older (A(s), B(s)) must have landed.
+  issue_a(0);
+  issue_b(0, 0);
+  if (nsteps > 1) issue_b(1, 1);
+  int bcur = 0;  // s % 3
+  for (int s = 0; s < ((abl & 8) ? 0 : nsteps); ++s) {
+    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // NB = 4
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();     // every wave's DMA of step s has landed; step s-1's reads are done
+    asm volatile("" ::: "memory");    // no LDS read moves above the barrier
+    if (!(abl & 1)) {
+    if (s + 1 < nsteps) issue_a(s + 1);
+    if (s + 2 < nsteps) issue_b(s + 2, bcur == 0 ? 2 : bcur - 1);  // (s + 2) % 3
+    }
+    const char* As = sm + (s & 1) * A_BYTES;
+    const char* Bs = sm + B_OFF + bcur * B_BYTES;
+    bcur = bcur == 2 ? 0 : bcur + 1;
     half8 ah[TM], al[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -123,17 +139,41 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       ah[i] = lds_frag(As, row, G);
       al[i] = lds_frag(As, row, G + 4);
     }
+    // B fragments one pixel group ahead: the reads of group j+1 are in flight while group j's 12
+    // MFMAs issue (both waves of a SIMD reach these waits together, so an exposed LDS latency
+    // idles the matrix pipe)
+    half8 bh[2], bl[2];
+    bh[0] = lds_frag(Bs, wn * WN + l16, G);
+    bl[0] = lds_frag(Bs, wn * WN + l16, G + 4);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = wn * WN + j * 16 + l16;
-      const half8 bh = lds_frag(Bs, n, G);
-      const half8 bl = lds_frag(Bs, n, G + 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][j], 0, 0, 0);
+      if (j + 1 < TN) {
+        const int n = wn * WN + (j + 1) * 16 + l16;
+        bh[(j + 1) & 1] = lds_frag(Bs, n, G);
+        bl[(j + 1) & 1] = lds_frag(Bs, n, G + 4);
       }
+      if (abl & 2) {
+        asm volatile("" :: "v"(bh[j & 1]), "v"(bl[j & 1]));
+        continue;
+      }
+      // term-major: consecutive MFMAs never chain on one accumulator
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j & 1], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j & 1], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
+    }
+    // pin that order (hipcc otherwise sinks each group's reads below the previous group's MFMAs and
+    // waits on them): A + first B reads, then per group its successor's 2 reads and its 12 MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM + 2, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j + 1 < TN) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);
     }
   }
 
@@ -142,24 +182,70 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   // col = pixel; per 16-row group the wave transposes to rows of WN pixels and stores each Cout row
   // as 128-byte runs.  Every acc index stays compile-time (a runtime-indexed acc goes to scratch).
   constexpr int EP = WN + 4;  // row pitch (floats): the 4 row groups of a write land on distinct banks
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (abl & 4) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
+  }
   float* ep = reinterpret_cast<float*>(sm) + wave * 16 * EP;
   const int co_w = ct * BM + wm * 64;
+  const bool shuf = (P.epi & EPI_SHUFFLE) != 0;
+  const bool vec = conv_vec_ok(P) && !(shuf && (P.epi & (EPI_GDN | EPI_IGDN | EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR)));
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) ep[(4 * G + e) * EP + j * 16 + l16] = acc[i][j][e];
+    // 16 rows x WN pixels -> 16-byte stores: 4 pixels of one Cout row, or under the pixel shuffle
+    // 2 pixels x the 2 channels that interleave along one output row
 #pragma unroll 1
-    for (int k = 0; k < 16 * WN / 64; ++k) {
+    for (int k = 0; k < WN / 16; ++k) {
       const int idx = k * 64 + lane;
-      const int r = idx / WN, n = idx % WN;
+      int r0, n;
+      float4 v;
+      if (!shuf) {
+        r0 = idx / (WN / 4);
+        n = 4 * (idx % (WN / 4));
+        v = *reinterpret_cast<const float4*>(ep + r0 * EP + n);
+      } else {
+        const int combo = idx / (WN / 2);  // (oc, dy) within the 16 rows
+        r0 = 4 * (combo >> 1) + 2 * (combo & 1);
+        n = 2 * (idx % (WN / 2));
+        const float2 c0 = *reinterpret_cast<const float2*>(ep + r0 * EP + n);
+        const float2 c1 = *reinterpret_cast<const float2*>(ep + (r0 + 1) * EP + n);
+        v = make_float4(c0.x, c1.x, c0.y, c1.y);
+      }
       const int nn = wn * WN + n;
       const int oy = oy0 + nn / TC, ox = ox0 + nn % TC;
-      const int co = co_w + i * 16 + r;
-      const float v = ep[r * EP + n];
-      if (oy < H && ox < W && co < P.Cout) conv_store(P, b, co, oy * W + ox, v);
+      const int co = co_w + i * 16 + r0;
+      if (oy >= H || ox >= W) continue;
+      const int p = oy * W + ox;
+      if (!shuf) {
+        if (vec && co < P.Cout && ox + 3 < W) {
+          conv_store4(P, b, co, p, v);
+        } else if (co < P.Cout) {
+          const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ox + e < W) conv_store(P, b, co, p + e, vs[e]);
+        }
+      } else {
+        if (vec && co + 1 < P.Cout && ox + 1 < W) {
+          conv_store_shuf4(P, b, co, p, v);
+        } else {
+          if (co < P.Cout) conv_store(P, b, co, p, v.x);
+          if (co + 1 < P.Cout) conv_store(P, b, co + 1, p, v.y);
+          if (ox + 1 < W) {
+            if (co < P.Cout) conv_store(P, b, co, p + 1, v.z);
+            if (co + 1 < P.Cout) conv_store(P, b, co + 1, p + 1, v.w);
+          }
+        }
+      }
     }
   }
 }
@@ -274,7 +360,11 @@ template <int K, int BM>
 static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st) {
   const int ntx = (P.W + TC - 1) / TC, nty = (P.H + TR - 1) / TR;
   dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B);
-  hipLaunchKernelGGL((conv_x4_kernel<K, BM>), grid, dim3(X4T), 0, st, P, act, wx, nchunk);
+  static const int abl = [] {
+    const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
+    return e ? std::atoi(e) : 0;
+  }();
+  hipLaunchKernelGGL((conv_x4_kernel<K, BM>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, abl);
   HIP_OK(hipGetLastError());
 }
 
