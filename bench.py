@@ -186,11 +186,10 @@ def main():
     rec = mdist.gather_records(rec.to(dev), max_per_rank=B).cpu()
     rec = rec[:, [F["bytes"], F["bpp_file"], F["psnr"]]]
 
-    # live roofline of the dominant kernel family: one extra profiled (untimed) step
+    # live roofline of the dominant kernel family: extra profiled (untimed) steps.  Pass 1 runs the
+    # timed steps' lane count, so its per-launch averages are what rocprofv3 sees over the whole run
+    # (concurrent lanes stretch each launch); pass 2 runs one lane: every launch alone on the GPU.
     h = net._handle
-    prof_lanes = a.profile_lanes or a.lanes
-    _lib.call("mlic_set_lanes", h, prof_lanes)
-    _lib.call("mlic_set_profiling", h, 1)
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
     names = []
@@ -198,13 +197,15 @@ def main():
         nb = C.create_string_buffer(128)
         _lib.call("mlic_profile_category_name", cat, nb, 128)
         names.append(nb.value.decode())
-    fam = {nm: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0} for nm in names}
-    layer_rows = []
-    phase_gpu = {}
 
-    def harvest(tag):
-        # per-layer table (before the reads, which clear), then per-family sums
-        if a.layers_out:
+    def profile_pass(lanes):
+        _lib.call("mlic_set_lanes", h, lanes)
+        _lib.call("mlic_set_profiling", h, 1)
+        fam = {nm: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0} for nm in names}
+        layer_rows, phase_gpu = [], {}
+
+        def harvest(tag):
+            # per-layer table (before the reads, which clear), then per-family sums
             n = C.c_size_t()
             _lib.call("mlic_profile_layers", h, None, 0, C.byref(n))
             buf = C.create_string_buffer(n.value + 1)
@@ -213,42 +214,50 @@ def main():
             if not layer_rows:
                 layer_rows.append("phase\t" + lines[0])
             layer_rows.extend(f"{tag}\t{ln}" for ln in lines[1:])
-        tot = 0.0
-        for cat, nm in enumerate(names):
-            n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
-            _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
-            f = fam[nm]
-            f["launches"] += n.value
-            f["ms"] += ms.value
-            f["flops"] += fl.value
-            f["bytes"] += by.value
-            tot += ms.value
-        phase_gpu[tag] = round(tot, 3)
+            tot = 0.0
+            for cat, nm in enumerate(names):
+                n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
+                _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
+                f = fam[nm]
+                f["launches"] += n.value
+                f["ms"] += ms.value
+                f["flops"] += fl.value
+                f["bytes"] += by.value
+                tot += ms.value
+            phase_gpu[tag] = round(tot, 3)
 
-    c = net.compress(x)
-    torch.cuda.synchronize()
-    harvest("compress")
-    net.decompress(c["strings"], c["shape"])
-    torch.cuda.synchronize()
-    harvest("decompress")
-    _lib.call("mlic_set_profiling", h, 0)
+        c = net.compress(x)
+        torch.cuda.synchronize()
+        harvest("compress")
+        net.decompress(c["strings"], c["shape"])
+        torch.cuda.synchronize()
+        harvest("decompress")
+        _lib.call("mlic_set_profiling", h, 0)
+        return fam, phase_gpu, layer_rows
+
+    prof_lanes = a.profile_lanes or a.lanes
+    fam, phase_gpu, layer_rows = profile_pass(prof_lanes)
+    fam1, phase_gpu1, layer_rows1 = profile_pass(1) if prof_lanes != 1 else (fam, phase_gpu, layer_rows)
     net.set_lanes(a.lanes)
     if a.layers_out and rank == 0:
-        with open(a.layers_out, "w") as f:
-            f.write("\n".join(layer_rows) + "\n")
+        with open(a.layers_out, "w") as f:  # isolated launches: the per-layer efficiency table
+            f.write("\n".join(layer_rows1) + "\n")
+
+    def roof(fam, dom):
+        conv = fam[dom]
+        peak_tf, arith = kernel_peak(dom)
+        sec = max(conv["ms"], 1e-9) * 1e-3
+        ai = conv["flops"] / max(conv["bytes"], 1.0)
+        if ai * PEAK_HBM_GBS * 1e9 < peak_tf * 1e12:
+            return "hbm", "GB/s", conv["bytes"] / sec / 1e9, PEAK_HBM_GBS, arith, conv
+        return "mfma", "TFLOP/s", conv["flops"] / sec / 1e12, peak_tf, arith, conv
+
     # dominant kernel = the conv kernel instantiation with the most device time; its roofline bound
     # is whichever ceiling is lower at its arithmetic intensity (algorithmic FLOPs / bytes)
     convs = [k for k in fam if is_conv(k)]
     dom = max(convs, key=lambda k: fam[k]["ms"])
-    conv = fam[dom]
-    peak_tf, arith = kernel_peak(dom)
-    sec = max(conv["ms"], 1e-9) * 1e-3
-    ai = conv["flops"] / max(conv["bytes"], 1.0)
-    hbm_bound = ai * PEAK_HBM_GBS * 1e9 < peak_tf * 1e12
-    if hbm_bound:
-        bound, unit, achieved, peak = "hbm", "GB/s", conv["bytes"] / sec / 1e9, PEAK_HBM_GBS
-    else:
-        bound, unit, achieved, peak = "mfma", "TFLOP/s", conv["flops"] / sec / 1e12, peak_tf
+    bound, unit, achieved, peak, arith, conv = roof(fam, dom)
+    _, _, achieved1, _, _, conv1 = roof(fam1, dom)
     conv_all = {k: sum(fam[c][k] for c in convs) for k in ("launches", "ms", "flops")}
     traffic = None
     try:
@@ -287,11 +296,17 @@ def main():
                          "avg_launch_us": round(1000 * conv["ms"] / max(1, conv["launches"]), 2),
                          "algorithmic_flops_per_launch": round(conv["flops"] / max(1, conv["launches"])),
                          "algorithmic_bytes_per_launch": round(conv["bytes"] / max(1, conv["launches"])),
-                         "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3)},
+                         "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3),
+                         # the same kernel family with every launch alone on the GPU (one lane)
+                         "isolated": {"achieved": round(achieved1, 3), "frac": round(achieved1 / peak, 4),
+                                      "launches_per_step": conv1["launches"],
+                                      "avg_launch_us": round(1000 * conv1["ms"] / max(1, conv1["launches"]), 2)}},
             # with profile_lanes > 1 these are per-launch durations summed over concurrently running lanes
             "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
             "gpu_kernel_ms_by_phase": phase_gpu,
+            "kernel_families_ms_per_step_isolated": {k: round(v["ms"], 3) for k, v in fam1.items() if v["launches"]},
+            "gpu_kernel_ms_per_step_isolated": round(sum(v["ms"] for v in fam1.values()), 3),
             "profile_lanes": prof_lanes,
             "host_thread_ms_per_step": host,
             "wall_ms_per_step": wall_split,

@@ -49,7 +49,8 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 
 template <int K, int BM>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
-                                                      const _Float16* __restrict__ wx, int nchunk, int abl) {
+                                                      const _Float16* __restrict__ wx, int nchunk, int H, int W,
+                                                      int abl) {
   constexpr int KK = K * K;
   constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WN = BN / WAVES_N;        // pixels per wave
@@ -63,7 +64,8 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int H = P.H, W = P.W, pad = K / 2;
+  const int pad = K / 2;  // H, W: the tiling grid (= P.H, P.W, or H*W folded into rows of 32 for K = 1)
+  const int npix = P.Ho * P.Wo;
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
   const int ntx = (W + TC - 1) / TC;
   const int nct = gridDim.x, npt = gridDim.y, nblk = nct * npt;
@@ -223,16 +225,16 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       const int nn = wn * WN + n;
       const int oy = oy0 + nn / TC, ox = ox0 + nn % TC;
       const int co = co_w + i * 16 + r0;
-      if (oy >= H || ox >= W) continue;
       const int p = oy * W + ox;
+      if (oy >= H || ox >= W || p >= npix) continue;
       if (!shuf) {
-        if (vec && co < P.Cout && ox + 3 < W) {
+        if (vec && co < P.Cout && ox + 3 < W && p + 3 < npix) {
           conv_store4(P, b, co, p, v);
         } else if (co < P.Cout) {
           const float vs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            if (ox + e < W) conv_store(P, b, co, p + e, vs[e]);
+            if (ox + e < W && p + e < npix) conv_store(P, b, co, p + e, vs[e]);
         }
       } else {
         if (vec && co + 1 < P.Cout && ox + 1 < W) {
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
 // activation packing: NCHW fp32 (multi-segment concat) -> act[b][chunk][Hp][Wp][hi 32 | lo 32]
 struct X4Pack {
   Seg seg[MAXSEG];
-  int nseg, Cin, H, W, pad, nchunk, square;
+  int nseg, Cin, H, W, pad, nchunk, square, npix;  // npix: real pixels (K = 1 folds H*W into rows of 32)
   _Float16* dst;
 };
 
@@ -266,12 +268,12 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   const int cc = blockIdx.y, b = blockIdx.z;
   if (pos >= Hp * Wp) return;
   const int y = pos / Wp - Q.pad, x = pos % Wp - Q.pad;
-  const bool inb = y >= 0 && y < Q.H && x >= 0 && x < Q.W;
+  const bool inb = y >= 0 && y < Q.H && x >= 0 && x < Q.W && y * Q.W + x < Q.npix;
   const int ch0 = cc * 32 + 8 * g;
   int s = 0, c0 = 0;  // 8-channel groups never straddle a segment (segments are 16-aligned)
   while (s + 1 < Q.nseg && ch0 >= c0 + Q.seg[s].C) { c0 += Q.seg[s].C; ++s; }
   const Seg sg = Q.seg[s];
-  const int64_t HW = (int64_t)Q.H * Q.W;
+  const int64_t HW = Q.npix;  // channel plane stride of the (unfolded) input
   const float* src = sg.p + (int64_t)b * sg.bs + (int64_t)(ch0 - c0) * HW + (int64_t)y * Q.W + x;
   half8 h, l;
 #pragma unroll
@@ -312,7 +314,11 @@ __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _F
 }
 
 // ---------------------------------------------------------------------------------------------
-int x4_bm(int Cout) { return Cout >= 192 ? 256 : 128; }
+// 256-row Cout tiles unless 128-row tiles pad at least 1/8 of Cout less (e.g. 320, 640 -> 128)
+int x4_bm(int Cout) {
+  const int w256 = (Cout + 255) / 256 * 256 - Cout, w128 = (Cout + 127) / 128 * 128 - Cout;
+  return (Cout >= 192 && 8 * (w256 - w128) <= Cout) ? 256 : 128;
+}
 
 int64_t x4_weight_halves(int Cout, int KK, int cin_pad) {
   const int bm = x4_bm(Cout);
@@ -327,9 +333,18 @@ void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, i
   HIP_OK(hipGetLastError());
 }
 
+// K = 1: no spatial coupling, so the flat pixel index is folded into rows of TC = 32: every
+// 8 x 32 tile is 256 consecutive pixels and only the image's last tile is ragged
+static void x4_grid(const ConvParams& P, int& H, int& W) {
+  H = P.K == 1 ? (P.H * P.W + TC - 1) / TC : P.H;
+  W = P.K == 1 ? TC : P.W;
+}
+
 int64_t x4_act_halves(const ConvParams& P, int cin_pad) {
   const int pad = P.K / 2;
-  return (int64_t)P.B * (cin_pad / 32) * (P.H + 2 * pad) * (P.W + 2 * pad) * ROWH;
+  int H, W;
+  x4_grid(P, H, W);
+  return (int64_t)P.B * (cin_pad / 32) * (H + 2 * pad) * (W + 2 * pad) * ROWH;
 }
 
 bool conv_x4_ok(const ConvParams& P, int cin_pad) {
@@ -345,26 +360,28 @@ void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st
   for (int s = 0; s < P.nseg; ++s) Q.seg[s] = P.seg[s];
   Q.nseg = P.nseg;
   Q.Cin = P.Cin;
-  Q.H = P.H;
-  Q.W = P.W;
+  x4_grid(P, Q.H, Q.W);
+  Q.npix = P.H * P.W;
   Q.pad = P.K / 2;
   Q.nchunk = cin_pad / 32;
   Q.square = (P.epi & EPI_SQUARE_IN) ? 1 : 0;
   Q.dst = dst;
-  const int npos = (P.H + 2 * Q.pad) * (P.W + 2 * Q.pad);
+  const int npos = (Q.H + 2 * Q.pad) * (Q.W + 2 * Q.pad);
   hipLaunchKernelGGL(x4_pack_act_kernel, dim3((npos + 63) / 64, Q.nchunk, P.B), dim3(256), 0, st, Q);
   HIP_OK(hipGetLastError());
 }
 
 template <int K, int BM>
 static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st) {
-  const int ntx = (P.W + TC - 1) / TC, nty = (P.H + TR - 1) / TR;
+  int H, W;
+  x4_grid(P, H, W);
+  const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
   dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B);
   static const int abl = [] {
     const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
     return e ? std::atoi(e) : 0;
   }();
-  hipLaunchKernelGGL((conv_x4_kernel<K, BM>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, abl);
+  hipLaunchKernelGGL((conv_x4_kernel<K, BM>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl);
   HIP_OK(hipGetLastError());
 }
 
