@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=24, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--model", default="MLICPP_L")
     ap.add_argument("--height", type=int, default=1088)
     ap.add_argument("--width", type=int, default=1920)

@@ -42,6 +42,15 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
+// The same DMA as an asm statement: hipcc cannot see that it writes LDS, so it does not wait for it
+// before the k-loop's own ds_reads of the other buffers (it would, conservatively, for the builtin).
+// Ordering is the caller's: counted vmcnt + barrier before any read of the destination buffer.
+__device__ __forceinline__ void glds16_asm(const void* src, const void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)lds));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(l) : "m0");
+}
+
 __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule) {
   return *reinterpret_cast<const half8*>(base + row * ROWB + ((granule ^ swz(row)) << 4));
 }
@@ -56,7 +65,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   constexpr int WN = BN / WAVES_N;        // pixels per wave
   constexpr int TM = 4, TN = WN / 16;     // 16x16 fragments per wave
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
-  constexpr int B_OFF = 2 * A_BYTES, LDS = 2 * A_BYTES + 3 * B_BYTES;
+  constexpr int B_OFF = 3 * A_BYTES, LDS = 3 * A_BYTES + 2 * B_BYTES;
   constexpr int NA = A_BYTES / 1024 / 8;  // 1 KB glds instructions per wave for A
   constexpr int NB = B_BYTES / 1024 / 8;  // ... for B
   static_assert(NA >= 1 && NB == 4 && LDS <= 160 * 1024, "x4 tile");
@@ -94,20 +103,20 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   }
   const _Float16* asrc = wx + ((int64_t)ct * nsteps * BM) * ROWH + (wave * NA) * 512 + lane * 8;
 
-  auto issue_a = [&](int s) {
-    char* st = sm + (s & 1) * A_BYTES;
-    const _Float16* a = asrc + (int64_t)s * BM * ROWH;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) glds16(a + i * 512, st + (wave * NA + i) * 1024);
+  // DMA instruction g of one step: g < NB moves the wave's B lines of step sb into B buffer sb & 1,
+  // g >= NB its A rows of step sa into A buffer abuf (B before A: the vmcnt accounting relies on it)
+  auto glds_one = [&](int g, int sb, int sa, int abuf) {
+    if (g < NB) {
+      const int cc = sb / KK, tap = sb - cc * KK;
+      const int ky = tap / K, kx = tap - ky * K;
+      const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
+      glds16_asm(bsrc[g] + d, sm + B_OFF + (sb & 1) * B_BYTES + (wave * NB + g) * 1024);
+    } else {
+      const int i = g - NB;
+      glds16_asm(asrc + (int64_t)sa * BM * ROWH + i * 512, sm + abuf * A_BYTES + (wave * NA + i) * 1024);
+    }
   };
-  auto issue_b = [&](int s, int buf) {
-    char* st = sm + B_OFF + buf * B_BYTES;
-    const int cc = s / KK, tap = s - cc * KK;
-    const int ky = tap / K, kx = tap - ky * K;
-    const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) glds16(bsrc[i] + d, st + (wave * NB + i) * 1024);
-  };
+  constexpr int NG = NA + NB;
 
   floatx4 acc[TM][TN];
 #pragma unroll
@@ -116,24 +125,27 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int G = lane >> 4, l16 = lane & 15;
-  // issue order: A0 B0 B1 | step 0: A1 B2 | step 1: A2 B3 | ...  At the top of step s the newest NB
-  // requests are B(s+1); everything older (A(s), B(s)) must have landed.
-  issue_a(0);
-  issue_b(0, 0);
-  if (nsteps > 1) issue_b(1, 1);
-  int bcur = 0;  // s % 3
+  // issue order: A0 B0 A1 | step 0: B1 A2 | step 1: B2 A3 | ...  Every step issues its NG DMA
+  // instructions (past the end they re-fetch the last step into buffers no longer read), spread over
+  // its pixel groups so the matrix pipe keeps running while the TA works through them.  At the top of
+  // step s the newest NA requests are A(s+1); everything older (B(s), A(s)) must have landed.
+#pragma unroll
+  for (int g = NB; g < NG; ++g) glds_one(g, 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < NB; ++g) glds_one(g, 0, 0, 0);
+#pragma unroll
+  for (int g = NB; g < NG; ++g) glds_one(g, 0, min(1, nsteps - 1), 1);
+  int acur = 0;  // s % 3
   for (int s = 0; s < ((abl & 8) ? 0 : nsteps); ++s) {
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // NB = 4
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (NA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     __builtin_amdgcn_s_barrier();     // every wave's DMA of step s has landed; step s-1's reads are done
     asm volatile("" ::: "memory");    // no LDS read moves above the barrier
-    if (!(abl & 1)) {
-    if (s + 1 < nsteps) issue_a(s + 1);
-    if (s + 2 < nsteps) issue_b(s + 2, bcur == 0 ? 2 : bcur - 1);  // (s + 2) % 3
-    }
-    const char* As = sm + (s & 1) * A_BYTES;
-    const char* Bs = sm + B_OFF + bcur * B_BYTES;
-    bcur = bcur == 2 ? 0 : bcur + 1;
+    const int sb = min(s + 1, nsteps - 1), sa = min(s + 2, nsteps - 1);
+    const int anext = acur == 0 ? 2 : acur - 1;  // (s + 2) % 3
+    const char* As = sm + acur * A_BYTES;
+    const char* Bs = sm + B_OFF + (s & 1) * B_BYTES;
+    acur = acur == 2 ? 0 : acur + 1;
     half8 ah[TM], al[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -149,6 +161,11 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     bl[0] = lds_frag(Bs, wn * WN + l16, G + 4);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+      if (!(abl & 1)) {
+#pragma unroll
+        for (int g = j * NG / TN; g < (j + 1) * NG / TN; ++g) glds_one(g, sb, sa, anext);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one DMA slice per pixel group, between its MFMA groups
       if (j + 1 < TN) {
         const int n = wn * WN + (j + 1) * 16 + l16;
         bh[(j + 1) & 1] = lds_frag(Bs, n, G);
@@ -169,14 +186,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       for (int i = 0; i < TM; ++i)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
     }
-    // pin that order (hipcc otherwise sinks each group's reads below the previous group's MFMAs and
-    // waits on them): A + first B reads, then per group its successor's 2 reads and its 12 MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM + 2, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if (j + 1 < TN) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);
-    }
+
   }
 
   // epilogue through a wave-private LDS strip (the stage buffers are free once every wave is past
