@@ -292,6 +292,53 @@ View Model::alloc(int C, int H, int W) {
 
 void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
                  const View* aux, const View* res) {
+  const ConvParams P = conv_params(ins, w, stride, pad, out, epi, aux, res);
+  run_conv(P, w, nullptr);
+}
+
+// two convs of one input (ResidualBlockUpsample's subpel_conv and upsample): on the x4 path the
+// split-fp16 packing of the input is done once for both
+void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View& out1, int epi1, const ConvW& w2,
+                      const View& out2, int epi2) {
+  const ConvParams P1 = conv_params(ins, w1, 1, w1.K / 2, out1, epi1, nullptr, nullptr);
+  const ConvParams P2 = conv_params(ins, w2, 1, w2.K / 2, out2, epi2, nullptr, nullptr);
+  const ConvWeights c1{w1.w, w1.wh, w1.wl, w1.cin_pad, w1.wx4}, c2{w2.w, w2.wh, w2.wl, w2.cin_pad, w2.wx4};
+  if (conv_select(P1, c1, precision_) != CONV_X4 || conv_select(P2, c2, precision_) != CONV_X4 ||
+      w1.cin_pad != w2.cin_pad || w1.K != w2.K) {
+    run_conv(P1, w1, nullptr);
+    run_conv(P2, w2, nullptr);
+    return;
+  }
+  const size_t m = L().arena.mark();
+  _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((conv_ws_bytes(CONV_X4, P1, c1) + 3) / 4));
+  timed(PCAT_ELEM, 0.0, 8.0 * L().B * P1.Cin * P1.H * P1.W, [&] { x4_pack_act(P1, w1.cin_pad, act, L().st); },
+        w1.name + ".__x4_pack");
+  run_conv(P1, w1, act);
+  run_conv(P2, w2, act);
+  L().arena.release(m);
+}
+
+// packed: the input already in x4's split layout (conv_pair); the impl is then necessarily x4
+void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed) {
+  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4};
+  const int impl = packed ? CONV_X4 : conv_select(P, cw, precision_);
+  const double outn = (double)P.B * w.Cout * P.Ho * P.Wo;
+  const double flops = 2.0 * outn * P.Cin * w.K * w.K;
+  const double bytes = 4.0 * ((double)P.B * P.Cin * P.H * P.W + (double)w.Cout * P.Cin * w.K * w.K +
+                              outn * (1 + (P.aux ? 1 : 0) + (P.res ? 1 : 0)));
+  if (packed) {
+    timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_x4_forward(P, packed, w.wx4, w.cin_pad, L().st); }, w.name);
+    return;
+  }
+  const int64_t wsb = conv_ws_bytes(impl, P, cw);
+  const size_t m = L().arena.mark();
+  void* ws = wsb > 0 ? static_cast<void*>(L().arena.alloc((wsb + 3) / 4)) : nullptr;
+  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st, ws); }, w.name);
+  L().arena.release(m);  // stream-ordered: the next user of this memory runs after the conv
+}
+
+ConvParams Model::conv_params(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out,
+                              int epi, const View* aux, const View* res) {
   ConvParams P{};
   MLIC_CHECK(!ins.empty() && (int)ins.size() <= MAXSEG, "conv inputs");
   P.nseg = (int)ins.size();
@@ -334,16 +381,7 @@ void Model::conv(const std::vector<View>& ins, const ConvW& w, int stride, int p
     P.epi |= EPI_RES;
   }
   P.B = L().B;
-  const double outn = (double)L().B * w.Cout * P.Ho * P.Wo;
-  const double flops = 2.0 * outn * cin * w.K * w.K;
-  const double bytes = 4.0 * ((double)L().B * cin * P.H * P.W + (double)w.Cout * cin * w.K * w.K + outn * (1 + (aux ? 1 : 0) + (res ? 1 : 0)));
-  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4};
-  const int impl = conv_select(P, cw, precision_);
-  const int64_t wsb = conv_ws_bytes(impl, P, cw);
-  const size_t m = L().arena.mark();
-  void* ws = wsb > 0 ? static_cast<void*>(L().arena.alloc((wsb + 3) / 4)) : nullptr;
-  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st, ws); }, w.name);
-  L().arena.release(m);  // stream-ordered: the next user of this memory runs after the conv
+  return P;
 }
 
 void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu) {
@@ -447,9 +485,8 @@ View Model::rbu(const View& x, const std::string& p) {
   View out = alloc(C, 2 * x.H, 2 * x.W);
   const size_t m = L().arena.mark();
   View ta = alloc(C, 2 * x.H, 2 * x.W);
-  conv({x}, a, 1, 1, ta, EPI_GELU | EPI_SHUFFLE);
   View tu = alloc(C, 2 * x.H, 2 * x.W);
-  conv({x}, u, 1, 1, tu, EPI_SHUFFLE);
+  conv_pair({x}, a, ta, EPI_GELU | EPI_SHUFFLE, u, tu, EPI_SHUFFLE);
   View tc = conv3x3({ta}, p + ".conv", 1, true, EPI_NONE);
   gdn(tc, p + ".igdn", true, out, &tu);
   L().arena.release(m);

@@ -194,6 +194,11 @@ class Model {
   View alloc(int C, int H, int W);
   void conv(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
             const View* aux = nullptr, const View* res = nullptr);
+  ConvParams conv_params(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
+                         const View* aux, const View* res);
+  void run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed);
+  void conv_pair(const std::vector<View>& ins, const ConvW& w1, const View& out1, int epi1, const ConvW& w2,
+                 const View& out2, int epi2);
   void dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu);
   View conv3x3(const std::vector<View>& ins, const std::string& p, int stride, bool dwsep, int epi,
                const View* res = nullptr, const View* out = nullptr);
