@@ -86,7 +86,8 @@ int mlic_profile_category_name(int cat, char* buf, size_t cap);
 
 /* kernel-level entry points (bit-exact tests, micro-benchmarks) */
 /* one conv layer with a given kernel family: impl -1 = the model's choice (precision 2), 0 fp32 MFMA,
- * 1 f16x3, 2 f16x3 v2, 3 resident-weight 1x1, 4 narrow 3x3, 5 small-Cin 1x1, 6 halo-tiled 3x3.  w is torch layout
+ * 1 f16x3, 2 f16x3 v2, 3 resident-weight 1x1, 4 narrow 3x3, 5 small-Cin 1x1, 6 halo-tiled 3x3,
+ * 7 x4 (split-fp16, both operands staged by LDS-DMA; K in 1, 3, 5, stride 1).  w is torch layout
  * [Cout][Cin][K][K]; pad = K/2; epi = Epi flags of common.h (aux for GDN, res for residual).
  * Synchronous on `stream`. */
 int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,
@@ -101,6 +102,10 @@ int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 2
 /* LocalContext window attention: qkv [B][3C][H*W] -> out [B][25C][H*W]; impl 0 = VALU, 1 = MFMA */
 int mlic_local_attn_run(void* stream, int impl, const float* qkv, const float* rel_table, const int32_t* rel_index,
                         float* out, int C, int H, int W, int B, float scale);
+/* LocalContext attention (dim 32) in conv_x4's packed split layout: out = uint16 (fp16 bits)
+   [B][25][npos][64], npos = ceil(H*W / 32) * 32; channel k = head*16 + d, hi at k, lo at 32 + k */
+int mlic_local_attn_packed_run(void* stream, const float* qkv, const float* rel_table, const int32_t* rel_index,
+                               uint16_t* out, int H, int W, int B, float scale);
 int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);
 int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out);
 

@@ -195,6 +195,162 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_mfma_kernel(LocalAttnPa
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// hd = 16 (MLICPP_L/M/S): the same attention, writing the fusion conv's B operand directly in
+// conv_x4's packed split layout  out[b][i][pos][64 halves]: chunk = query cell i (25 chunks),
+// channel k = head*16 + d (hi at k, lo at 32 + k), pos = flat pixel (K = 1 folding of conv_x4).
+// The fusion weights are permuted to that order once at load (k' = i*32 + head*16 + d), so the
+// 5x5 "fusion" conv runs on conv_x4 with no fp32 round trip of the 800-row map and no packing pass.
+// Both heads are processed in one pass (two independent MFMA / softmax chains per pixel); loads
+// are branch-free (lanes outside the 25-cell window read a zero cell), q is pre-scaled at staging.
+namespace {
+constexpr int LP_TW = 32, LP_LW = LP_TW + 4, LP_NCELL = 5 * LP_LW, LP_NCP = LP_NCELL + 1;
+}
+
+__global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttnParams P, _Float16* __restrict__ outp,
+                                                                     int npos) {
+  __shared__ __attribute__((aligned(16))) float sm[3 * 32 * LP_NCP];  // q*scale | k | v, [ch][cell]
+  const int H = P.H, W = P.W, HW = H * W;
+  const int b = blockIdx.y;
+  const int ntx = (W + LP_TW - 1) / LP_TW;
+  const int x0 = (blockIdx.x % ntx) * LP_TW, y0 = blockIdx.x / ntx;
+  const float* src = P.qkv + (int64_t)b * P.qkv_bs;
+  for (int i = threadIdx.x; i < 3 * 32 * LP_NCP; i += LA_THREADS) {
+    const int ch = i / LP_NCP, cell = i - ch * LP_NCP;
+    float v = 0.0f;
+    if (cell < LP_NCELL) {
+      const int gy = y0 - 2 + cell / LP_LW, gx = x0 - 2 + cell % LP_LW;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = src[(int64_t)ch * HW + gy * W + gx];
+      if (ch < 32) v *= P.scale;
+    }
+    sm[i] = v;
+  }
+  __syncthreads();
+  const float* qs = sm;
+  const float* ks = sm + 32 * LP_NCP;
+  const float* vs = sm + 64 * LP_NCP;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const bool lvalid = l32 < 25;
+  const int cy = lvalid ? l32 / 5 : 0, cx = lvalid ? l32 % 5 : 0;
+  // relative-position bias (query i = l32, key j of register r), both heads
+  float bias[2][16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      bias[hh][r] = (lvalid && j < 25) ? P.rel_table[P.rel_index[l32 * 25 + j] * 2 + hh] : 0.0f;
+  }
+  // V^T gather: key j of element e of k-step t, as a window-cell offset (-1: outside the window)
+  int voff[2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = 16 * t + 8 * (e >> 2) + 4 * h + (e & 3);
+      voff[t][e] = (j < 25 && l32 < 16) ? (j / 5) * LP_LW + (j % 5) : -1;
+    }
+
+  for (int lx = wave; lx < LP_TW; lx += LA_WAVES) {
+    const int px = x0 + lx, py = y0;
+    if (px >= W) break;  // wave-uniform
+    const int qcell = lvalid ? cy * LP_LW + lx + cx : LP_NCELL;
+    const int par = py + px;
+    const int qgy = py + cy - 2, qgx = px + cx - 2;
+    const bool qa = lvalid && qgy >= 0 && qgy < H && qgx >= 0 && qgx < W && ((par + cy + cx) & 1);
+    floatx16 sacc[2], oacc[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      // S^T = K Q^T over the 16 head dims (lane half h holds dims 8h .. 8h+7); channel = d*2 + head
+      float kv[8], qv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = (8 * h + e) * 2 + hh;
+        kv[e] = ks[ch * LP_NCP + qcell];
+        qv[e] = qs[ch * LP_NCP + qcell];
+      }
+      half8 kh_, kl_, qh_, ql_;
+      split8(kv, kh_, kl_);
+      split8(qv, qh_, ql_);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[hh][r] = 0.0f;
+      sacc[hh] = mfma3(kh_, kl_, qh_, ql_, sacc[hh]);
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int jy = j / 5, jx = j - 5 * (j / 5);
+        const int kgy = py + jy - 2, kgx = px + jx - 2;
+        const bool ka = kgy >= 0 && kgy < H && kgx >= 0 && kgx < W && ((par + jy + jx) & 1);
+        const float v = sacc[hh][r] + bias[hh][r] + ((qa && ka) ? 0.0f : -100.0f);
+        sacc[hh][r] = j < 25 ? v : -3.0e38f;
+        mx = fmaxf(mx, sacc[hh][r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sum = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+        sacc[hh][r] = j < 25 ? expf(sacc[hh][r] - mx) : 0.0f;
+        sum += sacc[hh][r];
+      }
+      sum += __shfl_xor(sum, 32);
+      const float inv = 1.0f / sum;
+      // O^T = V^T P^T (k = keys; P^T registers 8t .. 8t+7 are k-step t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[hh][r] = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        float pv[8], vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pv[e] = sacc[hh][8 * t + e] * inv;
+          const int c = voff[t][e];
+          vv[e] = vs[(l32 * 2 + hh) * LP_NCP + (c >= 0 ? c + lx : LP_NCELL)];
+        }
+        half8 ph, pl_, vh, vl;
+        split8(pv, ph, pl_);
+        split8(vv, vh, vl);
+        oacc[hh] = mfma3(vh, vl, ph, pl_, oacc[hh]);
+      }
+    }
+    // O^T[d][i]: registers 0..3 are d = 4h .. 4h+3, registers 4..7 are d = 8 + 4h .. +3 of query i
+    if (lvalid) {
+      typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+      _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + (int64_t)py * W + px) * 64;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          half4 hi, lo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = oacc[hh][4 * g + e];
+            const _Float16 hv = (_Float16)v;
+            hi[e] = hv;
+            lo[e] = (_Float16)(v - (float)hv);
+          }
+          const int k = hh * 16 + 8 * g + 4 * h;
+          *reinterpret_cast<half4*>(dst + k) = hi;
+          *reinterpret_cast<half4*>(dst + 32 + k) = lo;
+        }
+    }
+  }
+}
+
+void local_attn_packed(const LocalAttnParams& P, _Float16* out, int npos, hipStream_t st) {
+  MLIC_CHECK(P.C == 32, "packed LocalContext attention: dim 32 (2 heads x 16)");
+  MLIC_CHECK(npos >= P.H * P.W, "packed output positions");
+  const int ntx = (P.W + LP_TW - 1) / LP_TW;
+  hipLaunchKernelGGL(local_attn_packed_kernel, dim3(ntx * P.H, P.B), dim3(LA_THREADS), 0, st, P, out, npos);
+  HIP_OK(hipGetLastError());
+}
+
 template <int HD>
 static void launch_la(const LocalAttnParams& P, hipStream_t st) {
   using T = LaTile<HD>;

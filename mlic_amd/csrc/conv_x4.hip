@@ -137,8 +137,10 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   for (int g = NB; g < NG; ++g) glds_one(g, 0, min(1, nsteps - 1), 1);
   int acur = 0;  // s % 3
   for (int s = 0; s < ((abl & 8) ? 0 : nsteps); ++s) {
+    static_assert(NA == 1 || NA == 2 || NA == 4, "vmcnt immediate");
     if constexpr (NA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (NA == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     __builtin_amdgcn_s_barrier();     // every wave's DMA of step s has landed; step s-1's reads are done
     asm volatile("" ::: "memory");    // no LDS read moves above the barrier
     const int sb = min(s + 1, nsteps - 1), sa = min(s + 2, nsteps - 1);
@@ -326,6 +328,7 @@ __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _F
 // ---------------------------------------------------------------------------------------------
 // 256-row Cout tiles unless 128-row tiles pad at least 1/8 of Cout less (e.g. 320, 640 -> 128)
 int x4_bm(int Cout) {
+  if (Cout <= 64) return 64;
   const int w256 = (Cout + 255) / 256 * 256 - Cout, w128 = (Cout + 127) / 128 * 128 - Cout;
   return (Cout >= 192 && 8 * (w256 - w128) <= Cout) ? 256 : 128;
 }
@@ -359,7 +362,7 @@ int64_t x4_act_halves(const ConvParams& P, int cin_pad) {
 
 bool conv_x4_ok(const ConvParams& P, int cin_pad) {
   if (!(P.K == 1 || P.K == 3 || P.K == 5) || P.stride != 1 || P.pad != P.K / 2) return false;
-  if (P.Ho != P.H || P.Wo != P.W || cin_pad % 32 != 0 || cin_pad < P.Cin || P.Cout < 64) return false;
+  if (P.Ho != P.H || P.Wo != P.W || cin_pad % 32 != 0 || cin_pad < P.Cin || P.Cout < 32) return false;
   for (int s = 0; s + 1 < P.nseg; ++s)
     if (P.seg[s].C % 16 != 0) return false;
   return true;
@@ -401,12 +404,17 @@ void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* w
   ConvParams Q = P;
   Q.epi &= ~EPI_SQUARE_IN;
   const int nchunk = cin_pad / 32;
-  const bool wide = x4_bm(P.Cout) == 256;
+  const int bm = x4_bm(P.Cout);
+#define MLIC_X4_BM(K)                                              \
+  (bm == 256 ? launch_x4<K, 256>(Q, act, wx, nchunk, st)           \
+   : bm == 128 ? launch_x4<K, 128>(Q, act, wx, nchunk, st)         \
+               : launch_x4<K, 64>(Q, act, wx, nchunk, st))
   switch (P.K) {
-    case 1: wide ? launch_x4<1, 256>(Q, act, wx, nchunk, st) : launch_x4<1, 128>(Q, act, wx, nchunk, st); break;
-    case 3: wide ? launch_x4<3, 256>(Q, act, wx, nchunk, st) : launch_x4<3, 128>(Q, act, wx, nchunk, st); break;
-    default: wide ? launch_x4<5, 256>(Q, act, wx, nchunk, st) : launch_x4<5, 128>(Q, act, wx, nchunk, st); break;
+    case 1: MLIC_X4_BM(1); break;
+    case 3: MLIC_X4_BM(3); break;
+    default: MLIC_X4_BM(5); break;
   }
+#undef MLIC_X4_BM
 }
 
 }  // namespace mlic

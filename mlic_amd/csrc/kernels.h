@@ -107,6 +107,9 @@ struct LocalAttnParams {
 void local_attn(const LocalAttnParams& P, hipStream_t st);       // MFMA (attn_local.hip) unless MLIC_LOCAL_ATTN_VALU=1
 void local_attn_mfma(const LocalAttnParams& P, hipStream_t st);
 void local_attn_valu(const LocalAttnParams& P, hipStream_t st);
+// dim 32 only: output in conv_x4's packed split layout [B][25 query cells][npos][64 halves]
+// (channel head*16 + d), the B operand of the fusion conv with its K permuted to cell*32 + channel
+void local_attn_packed(const LocalAttnParams& P, _Float16* out, int npos, hipStream_t st);
 
 void softmax_spatial(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int mask_mode,
                      hipStream_t st);

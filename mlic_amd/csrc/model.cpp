@@ -121,6 +121,8 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
         MLIC_CHECK(shape(i, 2) == shape(i, 3), "square kernels only");
       }
       pack_conv(ptrs[i], dst, w.Cout, w.Cin, w.K * w.K, st);
+      if (k.find("local_context") != std::string::npos && ends_with(k, ".fusion.weight") && w.Cin == 800)
+        add_fusion_x4(base, ptrs[i], w.Cout, st);
       if (w.Cin >= 16) {  // split-fp16 copy for the f16x3 MFMA path
         w.cin_pad = (w.Cin + 31) / 32 * 32;
         const int64_t nh = (int64_t)w.Cout * w.K * w.K * w.cin_pad;
@@ -137,7 +139,8 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
   }
   // biases
   for (auto& kv : convs_) {
-    auto it = raw_.find(kv.first + ".bias");
+    const std::string b = ends_with(kv.first, ".__x4perm") ? kv.first.substr(0, kv.first.size() - 9) : kv.first;
+    auto it = raw_.find(b + ".bias");
     if (it != raw_.end()) kv.second.b = it->second;
   }
   for (auto& kv : dws_) {
@@ -208,6 +211,43 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
   MLIC_CHECK(raw_.count("__scale_table"), "scale table missing");
   scale_table_ = const_cast<float*>(raw_["__scale_table"]);
   HIP_OK(hipStreamSynchronize(st));
+}
+
+// LocalContext's 5x5 fusion conv over the unfolded attention map (K index c*25 + cell, c = head*16 +
+// d) as a conv_x4 GEMM over local_attn_packed's layout: K permuted to cell*32 + c, split, x4-packed
+void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout, hipStream_t st) {
+  constexpr int CIN = 800;
+  std::vector<float> w((size_t)Cout * CIN), wp((size_t)Cout * CIN);
+  HIP_OK(hipMemcpyAsync(w.data(), w_dev, w.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  for (int co = 0; co < Cout; ++co)
+    for (int c = 0; c < 32; ++c)
+      for (int cell = 0; cell < 25; ++cell) wp[(size_t)co * CIN + cell * 32 + c] = w[(size_t)co * CIN + c * 25 + cell];
+  const int64_t nh = (int64_t)Cout * CIN, nx = x4_weight_halves(Cout, 1, CIN);
+  char* blk = nullptr;
+  const size_t bytes = (size_t)nh * 4 + 2 * (size_t)nh * 2 + (size_t)nx * 2 + 1024;
+  HIP_OK(hipMalloc(&blk, bytes));
+  owned_.push_back(blk);
+  wbytes_ += bytes;
+  float* wf = reinterpret_cast<float*>(blk);
+  _Float16* wh = reinterpret_cast<_Float16*>(blk + (size_t)nh * 4);
+  _Float16* wl = wh + nh;
+  _Float16* wx = reinterpret_cast<_Float16*>((reinterpret_cast<uintptr_t>(wl + nh) + 255) & ~(uintptr_t)255);
+  HIP_OK(hipMemcpyAsync(wf, wp.data(), wp.size() * 4, hipMemcpyHostToDevice, st));
+  split_weights(wf, wh, wl, Cout, CIN, 1, CIN, st);
+  x4_pack_weights(wh, wl, Cout, 1, CIN, wx, st);
+  HIP_OK(hipStreamSynchronize(st));  // the host staging vectors die here
+  ConvW cw;
+  cw.w = wf;  // [Cout][800'] (not the fp32-MFMA packed layout: this ConvW only runs on conv_x4)
+  cw.Cout = Cout;
+  cw.Cin = CIN;
+  cw.K = 1;
+  cw.wh = wh;
+  cw.wl = wl;
+  cw.cin_pad = CIN;
+  cw.wx4 = wx;
+  cw.name = base;
+  convs_[base + ".__x4perm"] = cw;
 }
 
 Model::~Model() {
@@ -571,6 +611,27 @@ View Model::local_context(const View& x, int i) {
     ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, L().B, L().st);
   }, p + ".norm1");
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
+  View f = alloc(2 * C, H, W);
+  if (precision_ == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm")) {
+    // attention straight into the fusion conv's packed split operand, fusion on conv_x4
+    const ConvW& fw = cw(p + ".fusion.__x4perm");
+    const int npos = (H * W + 31) / 32 * 32;
+    _Float16* tp = reinterpret_cast<_Float16*>(L().arena.alloc((int64_t)L().B * 25 * npos * 32));
+    LocalAttnParams A{};
+    A.qkv = qkv.p;
+    A.qkv_bs = qkv.bs;
+    A.rel_table = rw(p + ".relative_position_table");
+    A.rel_index = rel_index_;
+    A.scale = (float)std::pow((double)(C / 2), -0.5);  // context.py:27 head_dim ** -0.5
+    A.C = C;
+    A.H = H;
+    A.W = W;
+    A.B = L().B;
+    const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
+    timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn_packed(A, tp, npos, L().st); }, p + ".attn");
+    const View tv{nullptr, 25 * C, H, W, (int64_t)25 * C * H * W};  // geometry only: conv_x4 reads tp
+    run_conv(conv_params({tv}, fw, 1, 0, f, EPI_NONE, nullptr, nullptr), fw, tp);
+  } else {
   View t = alloc(25 * C, H, W);
   {
     LocalAttnParams A{};
@@ -589,7 +650,8 @@ View Model::local_context(const View& x, int i) {
     const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
     timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn(A, L().st); }, p + ".attn");
   }
-  View f = conv1x1(t, p + ".fusion", 1, EPI_NONE);
+  conv({t}, cw(p + ".fusion"), 1, 0, f, EPI_NONE);
+  }
   View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
   View n2 = alloc(2 * C, H, W);
   timed(PCAT_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {

@@ -143,6 +143,8 @@ def test_halo_k1_k5(shape):
     (2, 960, 320, 17, 30, 1, GELU),             # 1x1 GEMM (entropy parameters), partial second tile
     (1, 288, 96, 13, 37, 5, 0),                 # 5x5 reprojection, 128-row tile
     (1, 480, 1920, 8, 16, 3, SHUFFLE | GELU),   # h_s subpel 480 -> 1920, 8 Cout tiles
+    (2, 800, 64, 17, 30, 1, RES),               # 64-row tile (LocalContext fusion), residual
+    (1, 128, 40, 9, 37, 1, 0),                  # Cout < 64, ragged folded pixel row
 ])
 def test_x4(shape):
     B, cin, cout, H, W, K, epi = shape
@@ -238,3 +240,30 @@ def test_local_attention_kernels(ch, H, W, B):
         d = (out - expect).abs()
         assert d.mean().item() <= 1e-5 * expect.abs().mean().item() + 1e-7, report
         assert d.max().item() <= 1e-3 * expect.abs().max().item(), report
+
+
+@pytest.mark.parametrize("H,W,B", [(24, 40, 2), (68, 120, 1), (13, 21, 1)])
+def test_local_attention_packed(H, W, B):
+    """The packed-output attention (dim 32) against the MFMA kernel's unfolded output: hi + lo of the
+    packed layout [B][cell][pos][64] re-ordered to row (head*16 + d)*25 + cell."""
+    from mlic_amd import _lib, synthetic
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    ch = 32
+    qkv = (torch.randn(B, 3 * ch, H, W, generator=g) * 2).to(dev)
+    table = torch.randn(81, 2, generator=g).to(dev)
+    index = torch.from_numpy(synthetic.relative_position_index(5)).reshape(-1).to(torch.int32).to(dev)
+    scale = 16 ** -0.5
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ref = torch.full((B, 25 * ch, H, W), float("nan"), device=dev)
+    _lib.call("mlic_local_attn_run", st, 1, C.c_void_p(qkv.data_ptr()), C.c_void_p(table.data_ptr()),
+              C.c_void_p(index.data_ptr()), C.c_void_p(ref.data_ptr()), ch, H, W, B, float(scale))
+    npos = (H * W + 31) // 32 * 32
+    out = torch.zeros(B, 25, npos, 64, dtype=torch.float16, device=dev)
+    _lib.call("mlic_local_attn_packed_run", st, C.c_void_p(qkv.data_ptr()), C.c_void_p(table.data_ptr()),
+              C.c_void_p(index.data_ptr()), C.c_void_p(out.data_ptr()), H, W, B, float(scale))
+    v = out[..., :32].float() + out[..., 32:].float()           # [B, cell, pos, channel]
+    v = v[:, :, :H * W].permute(0, 3, 1, 2).reshape(B, 25 * ch, H, W)  # row channel*25 + cell
+    assert torch.isfinite(v).all()
+    d = (v - ref).abs()
+    assert d.max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, d.max().item()
