@@ -300,47 +300,49 @@ void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16
 }
 
 // ---------------------------------------------------------------------------------------------
-// 3x3 stride-1 pad-1 conv, Cout = COUT <= 16, exact fp32 on the VALU.
-constexpr int NR_TH = 16, NR_TW = 32, NR_CC = 8;
-constexpr int NR_PH = NR_TH + 2, NR_PW = NR_TW + 2;  // input patch (pitch NR_PW, even => 8-byte reads)
-constexpr int NR_PATCH = NR_CC * NR_PH * NR_PW;
-constexpr int NR_STAGE = (NR_PATCH + 255) / 256;
+// 3x3 stride-1 pad-1 conv, Cout = COUT <= 16, exact fp32 on the VALU (packed v_pk_fma_f32).
+// Tile 16 rows x 128 columns, 256 threads, each thread one row of 8 pixels x COUT outputs (4 pixel
+// pairs x COUT float2 accumulators), so every broadcast weight read (w, w, w', w') feeds 8 packed
+// FMAs.  Input staged per 2-channel chunk (LDS for 2 blocks / CU) with aligned float4 loads (patch column 0 = input column
+// ow0 - 4), weights per chunk as duplicated pairs; both double-buffered in LDS.  Outputs leave as
+// 16-byte stores (4 pixels of a channel, or under the pixel shuffle 2 pixels x 2 channels).
+constexpr int NR_TH = 16, NR_TW = 128, NR_CC = 2;
+constexpr int NR_PH = NR_TH + 2, NR_PQ = NR_TW / 4 + 2;  // patch rows, float4 per patch row
+constexpr int NR_PITCH = NR_PQ * 4;                      // floats
+constexpr int NR_PATCH4 = NR_CC * NR_PH * NR_PQ;         // float4 per chunk patch
+constexpr int NR_STAGE = (NR_PATCH4 + 255) / 256;
 
 template <int COUT>
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
   typedef float float2v __attribute__((ext_vector_type(2)));
   typedef float float4v __attribute__((ext_vector_type(4)));
-  // per chunk: the input patch and the chunk's weights as duplicated (w, w) pairs, so one
-  // broadcast ds_read_b128 yields the packed operands of two v_pk_fma_f32 (2 pixels x 2 Cout)
-  constexpr int NW = NR_CC * 9 * COUT;  // weights per chunk
+  constexpr int NW = NR_CC * 9 * COUT / 2;  // (w, w, w', w') float4 per chunk
   static_assert(COUT % 2 == 0, "Cout pairs");
-  __shared__ __attribute__((aligned(16))) float sm[2 * NR_PATCH];
-  __shared__ __attribute__((aligned(16))) float4v swp[2][NW / 2];  // [c][tap][co pair] -> (w0, w0, w1, w1)
+  __shared__ __attribute__((aligned(16))) float4v sp[2][NR_PATCH4];
+  __shared__ __attribute__((aligned(16))) float4v swp[2][NW];
   const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;  // 2 output pixels (2tx, 2tx+1) of row ty
+  const int tx = tid & 15, ty = tid >> 4;  // pixels ow0 + 8 tx .. + 7 of row oh0 + ty
   const int ow0 = blockIdx.x * NR_TW, oh0 = blockIdx.y * NR_TH;
   const int b = blockIdx.z;
-  const int H = P.H, W = P.W;
+  const int H = P.H, W = P.W, W4 = W >> 2;
   const int64_t HW = (int64_t)H * W;
-  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs;
+  const float4v* x4 = reinterpret_cast<const float4v*>(P.seg[0].p + (int64_t)b * P.seg[0].bs);
   const int nchunk = (P.Cin + NR_CC - 1) / NR_CC;
   const float* w = P.wpk;  // [9][Cin][COUT]
-  constexpr int WSTAGE = (NW / 2 + 255) / 256;
+  constexpr int WSTAGE = (NW + 255) / 256;
 
-  float stage[NR_STAGE];
+  float4v stage[NR_STAGE];
   float4v wst[WSTAGE];
   auto load = [&](int ch) {
 #pragma unroll
     for (int s = 0; s < NR_STAGE; ++s) {
       const int e = tid + s * 256;
-      float v = 0.0f;
-      if (e < NR_PATCH) {
-        const int c = e / (NR_PH * NR_PW);
-        const int rem = e - c * (NR_PH * NR_PW);
-        const int py = rem / NR_PW, px = rem - py * NR_PW;
-        const int ci = ch * NR_CC + c;
-        const int ih = oh0 + py - 1, iw = ow0 + px - 1;
-        if (ci < P.Cin && ih >= 0 && ih < H && iw >= 0 && iw < W) v = x[(int64_t)ci * HW + (int64_t)ih * W + iw];
+      float4v v = {0.f, 0.f, 0.f, 0.f};
+      if (e < NR_PATCH4) {
+        const int c = e / (NR_PH * NR_PQ), rem = e - c * (NR_PH * NR_PQ);
+        const int py = rem / NR_PQ, pq = rem - py * NR_PQ;
+        const int ci = ch * NR_CC + c, ih = oh0 + py - 1, iq = (ow0 >> 2) - 1 + pq;
+        if (ci < P.Cin && ih >= 0 && ih < H && iq >= 0 && iq < W4) v = x4[(ci * HW >> 2) + (int64_t)ih * W4 + iq];
       }
       stage[s] = v;
     }
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
     for (int s = 0; s < WSTAGE; ++s) {
       const int e = tid + s * 256;  // (c, tap, co pair)
       float4v v = {0.f, 0.f, 0.f, 0.f};
-      if (e < NW / 2) {
+      if (e < NW) {
         const int c = e / (9 * COUT / 2), rem = e - c * (9 * COUT / 2);
         const int tap = rem / (COUT / 2), cp = rem - tap * (COUT / 2);
         const int ci = ch * NR_CC + c;
@@ -364,18 +366,20 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
 #pragma unroll
     for (int s = 0; s < NR_STAGE; ++s) {
       const int e = tid + s * 256;
-      if (e < NR_PATCH) sm[buf * NR_PATCH + e] = stage[s];
+      if (e < NR_PATCH4) sp[buf][e] = stage[s];
     }
 #pragma unroll
     for (int s = 0; s < WSTAGE; ++s) {
       const int e = tid + s * 256;
-      if (e < NW / 2) swp[buf][e] = wst[s];
+      if (e < NW) swp[buf][e] = wst[s];
     }
   };
 
-  float2v acc[COUT];
+  float2v acc[COUT][4];
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) acc[co] = float2v{0.0f, 0.0f};
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[co][q] = float2v{0.0f, 0.0f};
 
   load(0);
   store(0);
@@ -383,22 +387,28 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
   for (int ch = 0; ch < nchunk; ++ch) {
     const int cur = ch & 1;
     if (ch + 1 < nchunk) load(ch + 1);
-    const float* pb = sm + cur * NR_PATCH + ty * NR_PW + 2 * tx;
+    const float* pb = reinterpret_cast<const float*>(sp[cur]) + ty * NR_PITCH + 8 * tx + 3;
     const int cmax = min(NR_CC, P.Cin - ch * NR_CC);
     for (int c = 0; c < cmax; ++c) {
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
-        const float2v x01 = *reinterpret_cast<const float2v*>(pb + c * NR_PH * NR_PW + dy * NR_PW);
-        const float2v x23 = *reinterpret_cast<const float2v*>(pb + c * NR_PH * NR_PW + dy * NR_PW + 2);
-        const float2v xs[3] = {x01, float2v{x01.y, x23.x}, x23};
+        // input columns 8tx-1 .. 8tx+8 <-> patch columns 8tx+3 .. 8tx+12
+        const float* rp = pb + (c * NR_PH + dy) * NR_PITCH;
+        const float4v m0 = *reinterpret_cast<const float4v*>(rp + 1);
+        const float4v m1 = *reinterpret_cast<const float4v*>(rp + 5);
+        const float xw[10] = {rp[0], m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, rp[9]};
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
           const float4v* wq = &swp[cur][(c * 9 + dy * 3 + dx) * (COUT / 2)];
 #pragma unroll
           for (int cp = 0; cp < COUT / 2; ++cp) {
             const float4v ww = wq[cp];  // all lanes read the same address: broadcast
-            acc[2 * cp] = __builtin_elementwise_fma(xs[dx], float2v{ww.x, ww.y}, acc[2 * cp]);
-            acc[2 * cp + 1] = __builtin_elementwise_fma(xs[dx], float2v{ww.z, ww.w}, acc[2 * cp + 1]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float2v xv = {xw[2 * q + dx], xw[2 * q + 1 + dx]};
+              acc[2 * cp][q] = __builtin_elementwise_fma(xv, float2v{ww.x, ww.y}, acc[2 * cp][q]);
+              acc[2 * cp + 1][q] = __builtin_elementwise_fma(xv, float2v{ww.z, ww.w}, acc[2 * cp + 1][q]);
+            }
           }
         }
       }
@@ -407,21 +417,42 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvParams P) {
     __syncthreads();
   }
 
-  const int oh = oh0 + ty;
-  if (oh >= P.Ho) return;
+  const int oh = oh0 + ty, ow = ow0 + 8 * tx;
+  if (oh >= P.Ho || ow >= P.Wo) return;
+  const int p = oh * P.Wo + ow;
+  const bool shuf = (P.epi & EPI_SHUFFLE) != 0;
+  const bool full = ow + 7 < P.Wo && conv_vec_ok(P) && !(P.epi & (EPI_GDN | EPI_IGDN | EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR));
+  if (full && !shuf) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int ow = ow0 + 2 * tx + q;
-    if (ow >= P.Wo) continue;
-    const int p = oh * P.Wo + ow;
+    for (int co = 0; co < COUT; ++co)
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) conv_store(P, b, co, p, q ? acc[co].y : acc[co].x);
+      for (int h4 = 0; h4 < 2; ++h4)
+        conv_store4(P, b, co, p + 4 * h4,
+                    make_float4(acc[co][2 * h4].x, acc[co][2 * h4].y, acc[co][2 * h4 + 1].x, acc[co][2 * h4 + 1].y));
+  } else if (full) {
+#pragma unroll
+    for (int cp = 0; cp < COUT / 2; ++cp)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        conv_store_shuf4(P, b, 2 * cp, p + 2 * q,
+                         make_float4(acc[2 * cp][q].x, acc[2 * cp + 1][q].x, acc[2 * cp][q].y, acc[2 * cp + 1][q].y));
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        if (ow + 2 * q + e >= P.Wo) continue;
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) conv_store(P, b, co, p + 2 * q + e, e ? acc[co][q].y : acc[co][q].x);
+      }
   }
 }
 
 bool conv_narrow_ok(const ConvParams& P) {
+  // float4 patch loads: W % 4 == 0 and 16-byte aligned channel planes
   return P.K == 3 && P.stride == 1 && P.pad == 1 && P.nseg == 1 && P.Cout == 12 && P.Ho == P.H && P.Wo == P.W &&
-         !(P.epi & EPI_SQUARE_IN);
+         !(P.epi & EPI_SQUARE_IN) && (P.W % 4) == 0 && ((int64_t)P.H * P.W) % 4 == 0 && (P.seg[0].bs % 4) == 0 &&
+         (reinterpret_cast<uintptr_t>(P.seg[0].p) % 16) == 0;
 }
 
 void conv_narrow_forward(const ConvParams& P, hipStream_t st) {

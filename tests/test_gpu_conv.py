@@ -83,7 +83,8 @@ def test_pw_resident_ragged_and_many_tiles():
 @pytest.mark.parametrize("epi", [0, SHUFFLE])
 def test_narrow(epi):
     check(*run(NARROW, 2, 192, 12, 40, 72, 3, epi=epi))
-    check(*run(NARROW, 1, 96, 12, 19, 45, 3, epi=epi))
+    check(*run(NARROW, 1, 96, 12, 19, 44, 3, epi=epi))    # W % 4 == 0 (float4 patch loads)
+    check(*run(NARROW, 1, 192, 12, 33, 200, 3, epi=epi))  # ragged 128-column tile
 
 
 @pytest.mark.parametrize("stride", [1, 2])
