@@ -91,8 +91,11 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
 // float4 loads (patch column 0 = input column ox0 - 4, so each float4 is wholly inside or outside
 // the image when W % 4 == 0), and each thread computes a 4x4 output block from a sliding 3-row
 // register window: 6 patch rows x (1 float4 + 2 scalars) LDS reads for 16 outputs.
-constexpr int DWF_TH = 32, DWF_TW = 128, DWF_PR = DWF_TH + 2, DWF_PQ = DWF_TW / 4 + 2;  // patch rows, float4s/row
+// RPT rows per thread: tile height 8 * RPT (32, or 24 where it pads less, e.g. the 68-row latent)
+constexpr int DWF_TW = 128, DWF_PQ = DWF_TW / 4 + 2;  // float4s per patch row
+template <int RPT>
 __global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
+  constexpr int DWF_TH = 8 * RPT, DWF_PR = DWF_TH + 2;
   __shared__ float4 tile[DWF_PR * DWF_PQ];
   const int c = blockIdx.y, b = blockIdx.z;
   const int ntx = (P.Wo + DWF_TW - 1) / DWF_TW;
@@ -126,13 +129,13 @@ __global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
     dst[1] = m.x; dst[2] = m.y; dst[3] = m.z; dst[4] = m.w;
     dst[5] = rp[5];
   };
-  load_row(4 * rg, win[0]);
-  load_row(4 * rg + 1, win[1]);
+  load_row(RPT * rg, win[0]);
+  load_row(RPT * rg + 1, win[1]);
   float* dst = P.out + (int64_t)b * P.out_bs + (int64_t)c * P.Ho * P.Wo;
   const int ox = ox0 + 4 * cg;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    load_row(4 * rg + r + 2, win[(r + 2) % 3]);
+  for (int r = 0; r < RPT; ++r) {
+    load_row(RPT * rg + r + 2, win[(r + 2) % 3]);
     float o[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
       if (P.gelu) v = gelu_erf(v);
       o[q] = v;
     }
-    const int oy = oy0 + 4 * rg + r;
+    const int oy = oy0 + RPT * rg + r;
     if (oy < P.Ho && ox < P.Wo)  // Wo % 4 == 0: a strip is wholly inside or outside
       *reinterpret_cast<float4*>(dst + (int64_t)oy * P.Wo + ox) = make_float4(o[0], o[1], o[2], o[3]);
   }
@@ -213,8 +216,14 @@ void dw3x3(const DwParams& P, hipStream_t st) {
   }
   MLIC_CHECK(tot == P.C, "dw segments");
   if (P.stride == 1 && aligned) {
-    const int ntx = (P.Wo + DWF_TW - 1) / DWF_TW, nty = (P.Ho + DWF_TH - 1) / DWF_TH;
-    hipLaunchKernelGGL(dw3x3_s1_vec_kernel, dim3(ntx * nty, P.C, P.B), dim3(256), 0, st, P);
+    const int ntx = (P.Wo + DWF_TW - 1) / DWF_TW;
+    // staged rows per tile column: tiles * (TH + 2), the smaller of TH = 32 and TH = 24
+    const int n32 = (P.Ho + 31) / 32, n24 = (P.Ho + 23) / 24;
+    if (n24 * 26 < n32 * 34) {
+      hipLaunchKernelGGL(dw3x3_s1_vec_kernel<3>, dim3(ntx * n24, P.C, P.B), dim3(256), 0, st, P);
+    } else {
+      hipLaunchKernelGGL(dw3x3_s1_vec_kernel<4>, dim3(ntx * n32, P.C, P.B), dim3(256), 0, st, P);
+    }
     HIP_OK(hipGetLastError());
     return;
   }

@@ -169,6 +169,7 @@ def test_auto_matches_selected_family():
 
 @pytest.mark.parametrize("shape", [
     (2, 192, 64, 256, 1, 0),   # vectorised stride-1 path, 2 x 2 tiles
+    (1, 64, 68, 120, 1, 1),    # latent grid: 24-row tiles (3 x 24 covers 68 rows), GELU
     (2, 192, 40, 100, 1, 1),   # W % 4 == 0, ragged tiles, GELU
     (1, 96, 37, 53, 1, 0),     # W % 4 != 0: generic path
     (2, 192, 64, 96, 2, 0),    # stride 2, vectorised path (W % 8 == 0)
