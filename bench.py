@@ -188,7 +188,8 @@ def main():
 
     # live roofline of the dominant kernel family: extra profiled (untimed) steps.  Pass 1 runs the
     # timed steps' lane count, so its per-launch averages are what rocprofv3 sees over the whole run
-    # (concurrent lanes stretch each launch); pass 2 runs one lane: every launch alone on the GPU.
+    # (concurrent lanes stretch each launch); pass 2 runs one lane's share of the batch on one lane:
+    # launches of exactly the same shapes, each alone on the GPU.
     h = net._handle
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
@@ -198,7 +199,7 @@ def main():
         _lib.call("mlic_profile_category_name", cat, nb, 128)
         names.append(nb.value.decode())
 
-    def profile_pass(lanes):
+    def profile_pass(lanes, xs):
         _lib.call("mlic_set_lanes", h, lanes)
         _lib.call("mlic_set_profiling", h, 1)
         fam = {nm: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0} for nm in names}
@@ -226,7 +227,7 @@ def main():
                 tot += ms.value
             phase_gpu[tag] = round(tot, 3)
 
-        c = net.compress(x)
+        c = net.compress(xs)
         torch.cuda.synchronize()
         harvest("compress")
         net.decompress(c["strings"], c["shape"])
@@ -236,8 +237,10 @@ def main():
         return fam, phase_gpu, layer_rows
 
     prof_lanes = a.profile_lanes or a.lanes
-    fam, phase_gpu, layer_rows = profile_pass(prof_lanes)
-    fam1, phase_gpu1, layer_rows1 = profile_pass(1) if prof_lanes != 1 else (fam, phase_gpu, layer_rows)
+    fam, phase_gpu, layer_rows = profile_pass(prof_lanes, x)
+    share = max(1, B // prof_lanes)
+    fam1, phase_gpu1, layer_rows1 = (profile_pass(1, x[:share]) if prof_lanes != 1
+                                     else (fam, phase_gpu, layer_rows))
     net.set_lanes(a.lanes)
     if a.layers_out and rank == 0:
         with open(a.layers_out, "w") as f:  # isolated launches: the per-layer efficiency table
@@ -297,16 +300,20 @@ def main():
                          "algorithmic_flops_per_launch": round(conv["flops"] / max(1, conv["launches"])),
                          "algorithmic_bytes_per_launch": round(conv["bytes"] / max(1, conv["launches"])),
                          "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3),
-                         # the same kernel family with every launch alone on the GPU (one lane)
+                         # the same kernel family, same launch shapes, every launch alone on the GPU
+                         # (one lane running one lane's share of the batch)
                          "isolated": {"achieved": round(achieved1, 3), "frac": round(achieved1 / peak, 4),
+                                      "images": share,
                                       "launches_per_step": conv1["launches"],
                                       "avg_launch_us": round(1000 * conv1["ms"] / max(1, conv1["launches"]), 2)}},
             # with profile_lanes > 1 these are per-launch durations summed over concurrently running lanes
             "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
             "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
             "gpu_kernel_ms_by_phase": phase_gpu,
-            "kernel_families_ms_per_step_isolated": {k: round(v["ms"], 3) for k, v in fam1.items() if v["launches"]},
-            "gpu_kernel_ms_per_step_isolated": round(sum(v["ms"] for v in fam1.values()), 3),
+            # one lane's share of the batch, every launch alone on the GPU (x lanes = one step's work)
+            "kernel_families_ms_isolated_share": {k: round(v["ms"], 3) for k, v in fam1.items() if v["launches"]},
+            "gpu_kernel_ms_isolated_share": round(sum(v["ms"] for v in fam1.values()), 3),
+            "isolated_share_images": share,
             "profile_lanes": prof_lanes,
             "host_thread_ms_per_step": host,
             "wall_ms_per_step": wall_split,
