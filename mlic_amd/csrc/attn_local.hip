@@ -207,9 +207,17 @@ namespace {
 constexpr int LP_TW = 32, LP_LW = LP_TW + 4, LP_NCELL = 5 * LP_LW, LP_NCP = LP_NCELL + 1;
 }
 
+// Operands are split once at staging (not per use): q (pre-scaled) and k as [head][hi|lo][cell][16 d]
+// (a lane's 8 dims of one cell are one 16-byte read per half), v as hi / lo planes [head*16 + d][cell]
+// gathered 2 bytes at a time straight into the fragment.  Interior pixels take the checkerboard /
+// window mask from per-lane bit masks (parity only); the two rows / columns at the border compute
+// the in-image tests.
 __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttnParams P, _Float16* __restrict__ outp,
                                                                      int npos) {
-  __shared__ __attribute__((aligned(16))) float sm[3 * 32 * LP_NCP];  // q*scale | k | v, [ch][cell]
+  constexpr int QKP = LP_NCP * 16;       // halves per (tensor, head, hi|lo) plane
+  constexpr int QK_H = 2 * 2 * 2 * QKP;  // q, k x heads x hi|lo
+  constexpr int VP = 32 * LP_NCP;        // halves per v plane (hi or lo)
+  __shared__ __attribute__((aligned(16))) _Float16 sm[QK_H + 2 * VP];
   const int H = P.H, W = P.W, HW = H * W;
   const int b = blockIdx.y;
   const int ntx = (W + LP_TW - 1) / LP_TW;
@@ -223,12 +231,18 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
       if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = src[(int64_t)ch * HW + gy * W + gx];
       if (ch < 32) v *= P.scale;
     }
-    sm[i] = v;
+    const _Float16 hv = (_Float16)v, lv = (_Float16)(v - (float)hv);
+    const int which = ch >> 5, c = ch & 31, d = c >> 1, hh = c & 1;  // channel = d * heads + head
+    if (which < 2) {
+      _Float16* dst = sm + ((which * 2 + hh) * 2) * QKP + cell * 16 + d;
+      dst[0] = hv;
+      dst[QKP] = lv;
+    } else {
+      sm[QK_H + (hh * 16 + d) * LP_NCP + cell] = hv;
+      sm[QK_H + VP + (hh * 16 + d) * LP_NCP + cell] = lv;
+    }
   }
   __syncthreads();
-  const float* qs = sm;
-  const float* ks = sm + 32 * LP_NCP;
-  const float* vs = sm + 64 * LP_NCP;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -236,14 +250,25 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
   const int cy = lvalid ? l32 / 5 : 0, cx = lvalid ? l32 % 5 : 0;
   // relative-position bias (query i = l32, key j of register r), both heads
   float bias[2][16];
+  // interior mask bits for pixel parity 0 / 1: register r allowed iff query and key cell are anchors
+  uint32_t kbits[2] = {0u, 0u}, jbits = 0u;
+  bool qok[2];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int jy = j / 5, jx = j - 5 * (j / 5);
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh)
       bias[hh][r] = (lvalid && j < 25) ? P.rel_table[P.rel_index[l32 * 25 + j] * 2 + hh] : 0.0f;
+    if (j < 25) {
+      jbits |= 1u << r;
+      kbits[(jy + jx + 1) & 1] |= 1u << r;  // (par + jy + jx) odd
+    }
   }
-  // V^T gather: key j of element e of k-step t, as a window-cell offset (-1: outside the window)
+  qok[0] = lvalid && ((cy + cx) & 1);
+  qok[1] = lvalid && !((cy + cx) & 1);
+  // V^T gather: key j of element e of k-step t, as a window-cell offset (-1: outside the window or
+  // a padding row d >= 16 of the 32-row fragment)
   int voff[2][8];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -252,51 +277,57 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
       const int j = 16 * t + 8 * (e >> 2) + 4 * h + (e & 3);
       voff[t][e] = (j < 25 && l32 < 16) ? (j / 5) * LP_LW + (j % 5) : -1;
     }
+  const int vrow = l32 & 15;
 
   for (int lx = wave; lx < LP_TW; lx += LA_WAVES) {
     const int px = x0 + lx, py = y0;
     if (px >= W) break;  // wave-uniform
     const int qcell = lvalid ? cy * LP_LW + lx + cx : LP_NCELL;
-    const int par = py + px;
-    const int qgy = py + cy - 2, qgx = px + cx - 2;
-    const bool qa = lvalid && qgy >= 0 && qgy < H && qgx >= 0 && qgx < W && ((par + cy + cx) & 1);
+    const int par = (py + px) & 1;
+    const bool interior = py >= 2 && py < H - 2 && px >= 2 && px < W - 2;  // wave-uniform
     floatx16 sacc[2], oacc[2];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      // S^T = K Q^T over the 16 head dims (lane half h holds dims 8h .. 8h+7); channel = d*2 + head
-      float kv[8], qv[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int ch = (8 * h + e) * 2 + hh;
-        kv[e] = ks[ch * LP_NCP + qcell];
-        qv[e] = qs[ch * LP_NCP + qcell];
-      }
-      half8 kh_, kl_, qh_, ql_;
-      split8(kv, kh_, kl_);
-      split8(qv, qh_, ql_);
+      // S^T = K Q^T over the 16 head dims (lane half h holds dims 8h .. 8h+7)
+      const _Float16* kp = sm + ((1 * 2 + hh) * 2) * QKP + qcell * 16 + 8 * h;
+      const _Float16* qp = sm + ((0 * 2 + hh) * 2) * QKP + qcell * 16 + 8 * h;
+      const half8 kh_ = *reinterpret_cast<const half8*>(kp), kl_ = *reinterpret_cast<const half8*>(kp + QKP);
+      const half8 qh_ = *reinterpret_cast<const half8*>(qp), ql_ = *reinterpret_cast<const half8*>(qp + QKP);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[hh][r] = 0.0f;
       sacc[hh] = mfma3(kh_, kl_, qh_, ql_, sacc[hh]);
     }
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      float mx = -3.0e38f;
+    // allowed(r): interior = parity bits; border = the in-image tests of the reference's unfold
+    uint32_t allow;
+    if (interior) {
+      allow = qok[par] ? kbits[par] : 0u;
+    } else {
+      const int qgy = py + cy - 2, qgx = px + cx - 2;
+      const bool qa = lvalid && qgy >= 0 && qgy < H && qgx >= 0 && qgx < W && ((par + cy + cx) & 1);
+      allow = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int jy = j / 5, jx = j - 5 * (j / 5);
         const int kgy = py + jy - 2, kgx = px + jx - 2;
         const bool ka = kgy >= 0 && kgy < H && kgx >= 0 && kgx < W && ((par + jy + jx) & 1);
-        const float v = sacc[hh][r] + bias[hh][r] + ((qa && ka) ? 0.0f : -100.0f);
-        sacc[hh][r] = j < 25 ? v : -3.0e38f;
+        allow |= (qa && ka && j < 25) ? (1u << r) : 0u;
+      }
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = sacc[hh][r] + bias[hh][r] + (((allow >> r) & 1u) ? 0.0f : -100.0f);
+        sacc[hh][r] = ((jbits >> r) & 1u) ? v : -3.0e38f;
         mx = fmaxf(mx, sacc[hh][r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       float sum = 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
-        sacc[hh][r] = j < 25 ? expf(sacc[hh][r] - mx) : 0.0f;
+        sacc[hh][r] = ((jbits >> r) & 1u) ? expf(sacc[hh][r] - mx) : 0.0f;
         sum += sacc[hh][r];
       }
       sum += __shfl_xor(sum, 32);
@@ -304,18 +335,20 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
       // O^T = V^T P^T (k = keys; P^T registers 8t .. 8t+7 are k-step t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[hh][r] = 0.0f;
+      const _Float16* vh_p = sm + QK_H + (hh * 16 + vrow) * LP_NCP;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        float pv[8], vv[8];
+        float pv[8];
+        half8 vh, vl;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           pv[e] = sacc[hh][8 * t + e] * inv;
-          const int c = voff[t][e];
-          vv[e] = vs[(l32 * 2 + hh) * LP_NCP + (c >= 0 ? c + lx : LP_NCELL)];
+          const int c = voff[t][e] >= 0 ? voff[t][e] + lx : LP_NCELL;
+          vh[e] = vh_p[c];
+          vl[e] = vh_p[VP + c];
         }
-        half8 ph, pl_, vh, vl;
+        half8 ph, pl_;
         split8(pv, ph, pl_);
-        split8(vv, vh, vl);
         oacc[hh] = mfma3(vh, vl, ph, pl_, oacc[hh]);
       }
     }
