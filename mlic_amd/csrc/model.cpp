@@ -612,7 +612,11 @@ View Model::local_context(const View& x, int i) {
   }, p + ".norm1");
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
   View f = alloc(2 * C, H, W);
-  if (precision_ == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm")) {
+  static const bool packed_on = [] {  // $MLIC_LA_PACKED=0: the unfolded fp32 path (A/B switch)
+    const char* e = std::getenv("MLIC_LA_PACKED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (packed_on && precision_ == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm")) {
     // attention straight into the fusion conv's packed split operand, fusion on conv_x4
     const ConvW& fw = cw(p + ".fusion.__x4perm");
     const int npos = (H * W + 31) / 32 * 32;
