@@ -93,6 +93,11 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// GDN / IGDN output: x * rsqrt(v) / x * sqrt(v) on the hardware v_rsq / v_sqrt (1 ulp; v >= beta > 0)
+__device__ __forceinline__ float gdn_apply(float x, float v, bool inverse) {
+  return inverse ? x * __builtin_amdgcn_sqrtf(v) : x * __builtin_amdgcn_rsqf(v);
+}
+
 __device__ __forceinline__ bool is_anchor(int h, int w) { return ((h + w) & 1) == 1; }
 
 // the shared conv epilogue: bias, activation/normalisation, masks, residual, (shuffled) store of
@@ -104,7 +109,7 @@ __device__ __forceinline__ void conv_store(const ConvParams& P, int b, int co, i
   if (epi & EPI_GELU) v = gelu_erf(v);
   if (epi & (EPI_GDN | EPI_IGDN)) {
     const float x = P.aux[(int64_t)b * P.aux_bs + (int64_t)co * HWo + p];
-    v = (epi & EPI_GDN) ? x * (1.0f / sqrtf(v)) : x * sqrtf(v);
+    v = gdn_apply(x, v, (epi & EPI_GDN) == 0);
   }
   if (epi & EPI_TANH_HALF) v = 0.5f * tanhf(v);
   int oh = 0, ow = 0;
@@ -150,7 +155,7 @@ __device__ __forceinline__ void conv_store4(const ConvParams& P, int b, int co, 
     const float4 x = *reinterpret_cast<const float4*>(P.aux + (int64_t)b * P.aux_bs + (int64_t)co * P.Ho * P.Wo + p);
     const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) a[e] = (epi & EPI_GDN) ? xs[e] * (1.0f / sqrtf(a[e])) : xs[e] * sqrtf(a[e]);
+    for (int e = 0; e < 4; ++e) a[e] = gdn_apply(xs[e], a[e], (epi & EPI_GDN) == 0);
   }
   if (epi & EPI_TANH_HALF) {
 #pragma unroll

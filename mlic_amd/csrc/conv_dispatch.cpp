@@ -15,6 +15,18 @@ static bool x4_on() {
   return on;
 }
 
+// kernel sizes x4 takes (digits of $MLIC_X4_K, default "3"): the A/B switch for 1x1 / 5x5 layers
+static bool x4_k_on(int K) {
+  static const int mask = [] {
+    const char* e = std::getenv("MLIC_X4_K");
+    int m = 0;
+    for (const char* c = e ? e : "3"; *c; ++c)
+      if (*c >= '0' && *c <= '9') m |= 1 << (*c - '0');
+    return m;
+  }();
+  return (mask >> K) & 1;
+}
+
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (conv_smallcin_ok(P)) return CONV_SMALLCIN;  // exact fp32 VALU, all precisions
   if (conv_narrow_ok(P)) return CONV_NARROW;      // exact fp32 VALU, all precisions
@@ -23,9 +35,12 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
   if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
   // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs) once the grid fills the chip
-  if (w.wx4 && x4_on() && P.K == 3 && P.Cout >= 192 && conv_x4_ok(P, w.cin_pad) &&
-      (int64_t)((P.Cout + 255) / 256) * ((P.W + 31) / 32) * ((P.H + 7) / 8) * P.B >= 256)
-    return CONV_X4;
+  if (w.wx4 && x4_on() && x4_k_on(P.K) && P.Cout >= (P.K == 3 ? 192 : 64) && conv_x4_ok(P, w.cin_pad)) {
+    const int bm = x4_bm(P.Cout);
+    const int64_t rows = P.K == 1 ? ((int64_t)P.H * P.W + 31) / 32 : P.H;
+    const int64_t cols = P.K == 1 ? 1 : (P.W + 31) / 32;
+    if ((int64_t)((P.Cout + bm - 1) / bm) * cols * ((rows + 7) / 8) * P.B >= 256) return CONV_X4;
+  }
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay
   if (P.K == 5 && conv_halo_ok(P, w.cin_pad) &&

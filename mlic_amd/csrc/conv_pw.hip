@@ -222,7 +222,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
           float v = acc[c][r];
           v += sb[c * 32 + (r & 3) + 8 * (r >> 2)];
           if (gelu) v = gelu_erf(v);
-          if (gdn) v = igdn ? xa[r] * sqrtf(v) : xa[r] * (1.0f / sqrtf(v));
+          if (gdn) v = gdn_apply(xa[r], v, igdn);
           v += xr[r];
           if (c * 32 + 32 <= P.Cout || co < P.Cout)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
