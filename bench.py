@@ -1,16 +1,26 @@
-"""MLIC++ encode+decode throughput on MI355X (BASELINE.json config 2).
+"""MLIC++ encode+decode throughput on MI355X (BASELINE.json configs 2-5).
 
-One step = compress() + decompress() of a batch of synthetic 1920x1088 images on each GPU with
-MLICPP_L (seeded conditioned weights; no checkpoints offline).  Images shard across ranks (one
-process per GPU, weak scaling); the only collective is an all_gather of fixed-size per-image
-records (bpp/PSNR/bytes) after the timed region — SURVEY §8(e).
+One step = compress() + decompress() (real rANS bitstreams) of every image of the workload on each
+GPU.  Images shard across ranks (one process per GPU); the only collective is an all_gather of
+fixed-size per-image records after the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B]
+    python bench.py [--config main|kodak|s1080|sd1080|kodak-sweep|vbr-mixed] [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel family (the MFMA implicit-GEMM
-conv, ~95 % of the FLOPs) measured live with HIP events on the executor's stream in an extra,
-untimed step; `cpu_baseline` times the CPU oracle (torch fp32, this box's cores) on one image.
+Workloads (weights: seeded realistic-rate sets, mlic_amd/synthetic.py RATE_LAMBDAS; no checkpoints
+offline; images: seeded synthetic):
+  main        config 2: MLICPP_L, 32 x 1920x1088 per GPU (weak scaling)        <- the default line
+  kodak       config 1 shape on the GPU: MLICPP_L, 64 x 768x512 per GPU (weak)
+  s1080       config 3: MLICPP_S, 32 x 1920x1088 per GPU (weak)
+  sd1080      config 3: MLICPP_M_SMALL_DEC, 32 x 1920x1088 per GPU (weak)
+  kodak-sweep config 4: MLICPP_L, 24 Kodak-size images (20 x 768x512 + 4 portrait 512x768) x 6
+              lambda stand-ins = 144 jobs, LPT-sharded over the ranks (strong scaling)
+  vbr-mixed   config 5: MLICPP_L_VBR, 2 x 3840x2176 + 6 x 1920x1088 per GPU, a VBR level per image
+              (weak scaling)
+Rank 0 prints ONE JSON line.  `roofline` is the kernel family with the most device time in the timed
+configuration, measured live with HIP events on the executor streams in an extra untimed step, plus
+`step_frac` = T_roof / T_meas over every kernel of the step; `cpu_baseline` times the
+CPU oracle (torch fp32 restatement + native rANS) on a bounded sample on this box's cores.
 """
 from __future__ import annotations
 
@@ -29,26 +39,42 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "images/sec (enc+dec) at 1920×1088 MLICPP_L, 1/2/4/8 GPU; bpp/PSNR Δ vs ref"
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
 # dense peak of the arithmetic each kernel family runs on (MI355X_MICROARCH.md): fp32 MFMA 157.3 TF;
 # the split-fp16 kernels issue 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of
-# fp32-equivalent work; the VALU conv kernels run exact fp32 FMAs (157.3 TF with packed FMA)
+# fp32-equivalent work; the VALU kernels run exact fp32 FMAs (157.3 TF with packed FMA)
 def kernel_peak(name: str):
-    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv_halo")):
-        return 2500.0 / 3, "3 x v_mfma_f32_32x32x16_f16 per fp32 product (split-fp16)"
-    if name.startswith("conv_x4"):
-        return 2500.0 / 3, "3 x v_mfma_f32_16x16x32_f16 per fp32 product (split-fp16, LDS-DMA staged)"
+    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv_halo", "conv_x4", "chain_")):
+        return 2500.0 / 3, "3 x fp16 MFMA per fp32 product (split-fp16)"
+    if name.startswith("local_attn"):
+        return 2500.0 / 3, "3 x fp16 MFMA per fp32 product (split-fp16)"
     if name.startswith("conv_mfma"):
         return 157.3, "v_mfma_f32_32x32x2_f32"
     return 157.3, "fp32 VALU FMA"
 
 
-def is_conv(name: str) -> bool:
-    return name.startswith(("conv", "pw_resident"))
+def family(cat_name: str) -> str:
+    """Kernel family = template name without its <...> instantiation (rocprof lists each one)."""
+    return cat_name.split("<")[0]
 
 
-METRIC = "images/sec (enc+dec) at 1920×1088 MLICPP_L, 1/2/4/8 GPU; bpp/PSNR Δ vs ref"
-PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense, exact f32)
-PEAK_HBM_GBS = 8000.0
+WORKLOADS = {
+    "main": dict(model="MLICPP_L", groups=[(1088, 1920, 32)], scaling="weak",
+                 desc="config 2: MLICPP_L compress+decompress of 1920x1088 images"),
+    "kodak": dict(model="MLICPP_L", groups=[(512, 768, 64)], scaling="weak",
+                  desc="config 1 shape on GPU: MLICPP_L compress+decompress of 768x512 (Kodak-size) images"),
+    "s1080": dict(model="MLICPP_S", groups=[(1088, 1920, 32)], scaling="weak",
+                  desc="config 3: MLICPP_S compress+decompress of 1920x1088 images"),
+    "sd1080": dict(model="MLICPP_M_SMALL_DEC", groups=[(1088, 1920, 32)], scaling="weak",
+                   desc="config 3: MLICPP_M_SMALL_DEC compress+decompress of 1920x1088 images"),
+    "kodak-sweep": dict(model="MLICPP_L", scaling="strong",
+                        desc="config 4: MLICPP_L 24 Kodak-size images x 6 lambda stand-ins, LPT-sharded"),
+    "vbr-mixed": dict(model="MLICPP_L_VBR", groups=[(2176, 3840, 2), (1088, 1920, 6)], scaling="weak",
+                      desc="config 5: MLICPP_L_VBR 4K + 1080p batch, one VBR level per image"),
+}
 
 
 def parse():
@@ -56,34 +82,89 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
-    ap.add_argument("--model", default="MLICPP_L")
-    ap.add_argument("--height", type=int, default=1088)
-    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--config", default="main", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="override the per-GPU batch of a single-group workload")
+    ap.add_argument("--rate", type=int, default=1,
+                    help="realistic-rate weight set (0..5, synthetic.RATE_LAMBDAS) of fixed-rate workloads; "
+                         "-1 = the round-1 high-rate set")
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("MLIC_LANES", "4")),
                     help="host threads x HIP streams per GPU for compress/decompress")
     ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "2")),
                     help="dense-conv arithmetic: 2 = split-fp16 MFMA v2 + specialised kernels, "
                          "1 = f16x3 v1 tiles, 0 = fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--layers-out", default="", help="write the per-layer conv timing table here")
+    ap.add_argument("--no-roofline", action="store_true", help="skip the profiled passes")
+    ap.add_argument("--layers-out", default="", help="write the per-layer timing table here")
+    ap.add_argument("--records-out", default="", help="write the gathered per-image records (JSON) here")
     ap.add_argument("--profile-lanes", type=int, default=0,
                     help="lanes of the profiled step (0 = same as --lanes, so its launches match the timed "
                          "steps' and rocprofv3's per-kernel averages; 1 = isolated per-kernel times)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
-                    help="PMC-derived HBM bytes per conv launch (written by tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
+                    help="PMC-derived HBM bytes per launch of the dominant family (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def psnr_u8(a: torch.Tensor, b: torch.Tensor) -> float:
-    """utils/utils.py:86-87 (clamp, *255, truncate) + utils/metrics.py:32-33."""
+# ------------------------------------------------------------------------------------------ jobs
+class Job:
+    __slots__ = ("id", "model", "rate", "H", "W", "seed", "level")
+
+    def __init__(self, id, model, rate, H, W, seed, level=-1):
+        self.id, self.model, self.rate, self.H, self.W, self.seed, self.level = id, model, rate, H, W, seed, level
+
+
+def build_jobs(a, rank: int, world: int):
+    """This rank's jobs and the global job count."""
+    from mlic_amd import dist as mdist
+    wl = WORKLOADS[a.config]
+    rate = None if a.rate < 0 else a.rate
+    if a.config == "kodak-sweep":
+        # 24 Kodak-size images (the set has 4 portrait members) x 6 weight sets = 144 jobs (SURVEY §8(d))
+        shapes = [(512, 768)] * 20 + [(768, 512)] * 4
+        alljobs = [Job(r * 24 + i, wl["model"], r, H, W, 2000 + i, r) for r in range(6) for i, (H, W) in enumerate(shapes)]
+        mine = mdist.lpt_shard([(j.H, j.W) for j in alljobs], world)[rank]
+        return [alljobs[i] for i in mine], len(alljobs)
+    groups = wl["groups"]
+    if a.batch > 0 and len(groups) == 1:
+        groups = [(groups[0][0], groups[0][1], a.batch)]
+    per_rank = sum(g[2] for g in groups)
+    rng = np.random.Generator(np.random.PCG64(77 + rank))
+    jobs, k = [], 0
+    vbr = a.config == "vbr-mixed"
+    vrate = 2 if rate is None else rate
+    for (H, W, n) in groups:
+        for _ in range(n):
+            level = int(rng.integers(0, 6)) if vbr else (-1 if rate is None else rate)
+            jobs.append(Job(rank * per_rank + k, wl["model"], vrate if vbr else rate, H, W, 1000 * rank + k, level))
+            k += 1
+    return jobs, per_rank * world
+
+
+def batches(jobs, max_pixels=32 * 1088 * 1920):
+    """Group jobs by (weights, shape) into batches of at most ~32 1080p images' worth of pixels."""
+    out = {}
+    for j in jobs:
+        out.setdefault((j.model, j.rate, j.H, j.W), []).append(j)
+    res = []
+    for key, js in sorted(out.items(), key=lambda kv: (str(kv[0][1]), kv[0][2], kv[0][3])):
+        cap = max(1, max_pixels // (key[2] * key[3]))
+        for i in range(0, len(js), cap):
+            res.append((key, js[i:i + cap]))
+    return res
+
+
+def psnr_from_mse(mse: float) -> float:
+    return 20 * math.log10(255.0) - 10 * math.log10(mse) if mse > 0 else 99.0
+
+
+def mse_u8(a: torch.Tensor, b: torch.Tensor):
+    """utils/utils.py:86-87 (clamp, *255, truncate) + utils/metrics.py:32-33, per image."""
     qa = (a.clamp(0, 1) * 255).to(torch.uint8).float()
     qb = (b.clamp(0, 1) * 255).to(torch.uint8).float()
-    mse = torch.mean((qa - qb) ** 2).item()
-    return 20 * math.log10(255.0) - 10 * math.log10(mse) if mse > 0 else float("inf")
+    return ((qa - qb) ** 2).flatten(1).mean(1).double().cpu().tolist()
 
 
-def cpu_baseline(model: str, H: int, W: int):
+# ------------------------------------------------------------------------------------------ CPU side
+def cpu_baseline(model: str, rate, H: int, W: int, level: int = -1):
     """Oracle (torch CPU fp32 restatement of the reference) enc+dec of one image, with the native
     rANS coder for the entropy-coding part; threads = this process's CPU affinity (<= 32)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -91,27 +172,48 @@ def cpu_baseline(model: str, H: int, W: int):
     from mlic_amd import entropy, synthetic
     cores = max(1, min(32, len(os.sched_getaffinity(0))))
     torch.set_num_threads(cores)
-    sd = synthetic.synth_state_dict(model, 0)
+    sd = synthetic.synth_state_dict(model, 0, rate=rate)
     m = ref.RefMLIC(model, sd)
     x = synthetic.synth_image(H, W, 0)
+    s = max(0, level)
     tables = entropy.gaussian_tables(entropy.get_scale_table())
     t0 = time.time()
-    st = m.compress_streams(x)
+    st = m.compress_streams(x, s=s)
     sym = torch.cat([p[0].reshape(-1) for p in st["phases"]]).numpy()
     idx = torch.cat([p[1].reshape(-1) for p in st["phases"]]).numpy()
     data = entropy.rans_encode(sym, idx, *tables[:3])
     dec = entropy.rans_decode(data, idx, *tables[:3])
-    # decoder network: phases fed from the decoded symbols
     offs = np.cumsum([0] + [p[0].numel() for p in st["phases"]])
     phase_syms = [torch.from_numpy(dec[offs[k]:offs[k + 1]]).reshape(st["phases"][k][0].shape)
                   for k in range(len(st["phases"]))]
-    m.decode_streams(st["z_symbols"], phase_syms)
+    m.decode_streams(st["z_symbols"], phase_syms, s=s)
     dt = time.time() - t0
     return {"value": round(1.0 / dt, 5), "unit": "images/sec (enc+dec)", "cores": cores, "kind": "port",
-            "sample": f"1 image {W}x{H} {model}: oracle torch-CPU fp32 encoder+decoder networks + native rANS, "
-                      f"{dt:.1f} s"}
+            "sample": f"1 image {W}x{H} {model} (rate set {rate}): oracle torch-CPU fp32 encoder+decoder "
+                      f"networks + native rANS, {dt:.1f} s"}
 
 
+def oracle_deltas(model: str, levels, H: int, W: int, gpu_nets, dev):
+    """Per-lambda bpp / PSNR delta vs the CPU oracle on one image (kodak-sweep): GPU forward vs oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mlic_ref_cpu as ref
+    from mlic_amd import synthetic
+    x = synthetic.synth_image(H, W, 2000)
+    out = {}
+    for r in levels:
+        o = ref.RefMLIC(model, synthetic.synth_state_dict(model, rate=r)).forward(x)
+        g = gpu_nets[r](x.to(dev))
+        bc = ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"], o["likelihoods"]["z_likelihoods"], H * W)
+        bg = ref.bpp_from_likelihoods(g["likelihoods"]["y_likelihoods"].cpu(), g["likelihoods"]["z_likelihoods"].cpu(),
+                                      H * W)
+        pc, pg = ref.psnr_uint8(x, o["x_hat"]), ref.psnr_uint8(x, g["x_hat"].cpu())
+        out[f"lambda_{synthetic.RATE_LAMBDAS[r]}"] = {"bpp_gpu": round(bg, 6), "bpp_cpu": round(bc, 6),
+                                                      "d_bpp": round(bg - bc, 7), "psnr_gpu": round(pg, 5),
+                                                      "psnr_cpu": round(pc, 5), "d_psnr_db": round(pg - pc, 6)}
+    return out
+
+
+# ------------------------------------------------------------------------------------------ main
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,30 +225,52 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # host cores per rank: the ranks of a node split its cores into contiguous slices (pinned), and the
+    # entropy-coder pool of each rank gets its slice ($MLIC_HOST_THREADS, read at first use)
+    nloc = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    cores = sorted(os.sched_getaffinity(0))
+    if nloc > 1 and len(cores) >= 2 * nloc:
+        k = len(cores) // nloc
+        cores = cores[local * k:(local + 1) * k]
+        os.sched_setaffinity(0, cores)
+    if "MLIC_HOST_THREADS" not in os.environ:
+        os.environ["MLIC_HOST_THREADS"] = str(max(2, min(16, len(cores))))
 
     from mlic_amd import _lib, get_model, synthetic
     from mlic_amd import dist as mdist
-    net = get_model(a.model)
-    net.load_state_dict(synthetic.synth_state_dict(a.model, 0))
-    net = net.to(dev).eval()
-    net.update()
-    net.set_lanes(a.lanes)
-    net.set_precision(a.precision)
-    B, H, W = a.batch, a.height, a.width
-    x = torch.cat([synthetic.synth_image(H, W, 1000 * rank + i) for i in range(B)]).to(dev)
+    wl = WORKLOADS[a.config]
+    jobs, n_jobs_total = build_jobs(a, rank, world)
+    groups = batches(jobs)
+
+    nets = {}
+    for (model, rate, _, _), _js in groups:
+        if (model, rate) not in nets:
+            n = get_model(model)
+            n.load_state_dict(synthetic.synth_state_dict(model, 0, rate=rate))
+            n = n.to(dev).eval()
+            n.update()
+            n.set_lanes(a.lanes)
+            n.set_precision(a.precision)
+            nets[(model, rate)] = n
+    # inputs resident in HBM before the timed region
+    xs = [torch.cat([synthetic.synth_image(j.H, j.W, j.seed) for j in js]).to(dev) for _, js in groups]
+    is_vbr = wl["model"].endswith("_VBR")
 
     split = {"compress": 0.0, "decompress": 0.0}
+    last = {}
 
     def step():
-        t_a = time.perf_counter()
-        c = net.compress(x)
-        torch.cuda.synchronize()
-        t_b = time.perf_counter()
-        d = net.decompress(c["strings"], c["shape"])
-        torch.cuda.synchronize()
-        split["compress"] += t_b - t_a
-        split["decompress"] += time.perf_counter() - t_b
-        return c, d
+        for gi, ((model, rate, H, W), js) in enumerate(groups):
+            net = nets[(model, rate)]
+            kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
+            t_a = time.perf_counter()
+            c = net.compress(xs[gi], **kw)
+            t_b = time.perf_counter()
+            d = net.decompress(c["strings"], c["shape"], **kw)
+            t_c = time.perf_counter()
+            split["compress"] += t_b - t_a
+            split["decompress"] += t_c - t_b
+            last[gi] = (c, d, (t_b - t_a) / len(js), (t_c - t_b) / len(js))
 
     for _ in range(a.warmup):
         step()
@@ -155,42 +279,133 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     hs = [C.c_double() for _ in range(3)]
-    _lib.call("mlic_host_stats", net._ensure_handle(dev), *[C.byref(v) for v in hs], 1)
+    for n in nets.values():
+        _lib.call("mlic_host_stats", n._ensure_handle(dev), *[C.byref(v) for v in hs], 1)
     split["compress"] = split["decompress"] = 0.0
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        c, d = step()
+        step()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    _lib.call("mlic_host_stats", net._handle, *[C.byref(v) for v in hs], 1)
-    host = {k: round(v.value / a.steps, 2) for k, v in zip(("rans_encode", "rans_decode", "gpu_wait"), hs)}
+    host = {"rans_encode": 0.0, "rans_decode": 0.0, "gpu_wait": 0.0}
+    for n in nets.values():
+        _lib.call("mlic_host_stats", n._handle, *[C.byref(v) for v in hs], 1)
+        for k, v in zip(host, hs):
+            host[k] += v.value / a.steps
+    host = {k: round(v, 2) for k, v in host.items()}
     wall_split = {k: round(1000 * v / a.steps, 2) for k, v in split.items()}
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # per-image records: the one collective (all_gather over RCCL/xGMI), mlic_amd.dist
+    # per-image records (mlic_amd.dist.RECORD_FIELDS): the one collective, all_gather over RCCL/xGMI
     F = {k: i for i, k in enumerate(mdist.RECORD_FIELDS)}
-    rec = torch.zeros(B, mdist.RECORD_LEN, dtype=torch.float64)
-    for i in range(B):
-        nbytes = len(c["strings"][0][i]) + len(c["strings"][1][i])
-        rec[i, F["job"]] = rank * B + i
-        rec[i, F["H"]], rec[i, F["W"]] = H, W
-        rec[i, F["bytes"]] = nbytes
-        rec[i, F["bpp_file"]] = 8.0 * nbytes / (H * W)
-        rec[i, F["psnr"]] = psnr_u8(x[i], d["x_hat"][i])
-    rec = mdist.gather_records(rec.to(dev), max_per_rank=B).cpu()
-    rec = rec[:, [F["bytes"], F["bpp_file"], F["psnr"]]]
+    rec = torch.zeros(len(jobs), mdist.RECORD_LEN, dtype=torch.float64)
+    r = 0
+    for gi, ((model, rate, H, W), js) in enumerate(groups):
+        c, d, enc_s, dec_s = last[gi]
+        net = nets[(model, rate)]
+        mses = mse_u8(xs[gi], d["x_hat"])
+        for i, j in enumerate(js):
+            nbytes = len(c["strings"][0][i]) + len(c["strings"][1][i])
+            yb, zb = net.likelihood_bits(i)
+            rec[r, F["job"]] = j.id
+            rec[r, F["H"]], rec[r, F["W"]] = H, W
+            rec[r, F["level"]] = j.level
+            rec[r, F["bytes"]] = nbytes
+            rec[r, F["bpp_file"]] = 8.0 * nbytes / (H * W)
+            rec[r, F["bpp_lik"]] = (yb + zb) / (H * W)
+            rec[r, F["mse"]] = mses[i]
+            rec[r, F["psnr"]] = psnr_from_mse(mses[i])
+            rec[r, F["enc_ms"]] = 1000 * enc_s
+            rec[r, F["dec_ms"]] = 1000 * dec_s
+            r += 1
+    max_per_rank = max(len(jobs), 1)
+    if distributed:
+        mx = torch.tensor([max_per_rank], device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        max_per_rank = int(mx.item())
+    allrec = mdist.gather_records(rec.to(dev), max_per_rank=max_per_rank).cpu()
+    assert allrec.shape[0] == n_jobs_total, (allrec.shape, n_jobs_total)
 
-    # live roofline of the dominant kernel family: extra profiled (untimed) steps.  Pass 1 runs the
-    # timed steps' lane count, so its per-launch averages are what rocprofv3 sees over the whole run
-    # (concurrent lanes stretch each launch); pass 2 runs one lane's share of the batch on one lane:
-    # launches of exactly the same shapes, each alone on the GPU.
-    h = net._handle
+    # live roofline: extra profiled (untimed) steps.  Pass 1 runs the timed steps' lane count, so its
+    # per-launch averages are what rocprofv3 sees over the whole run (concurrent lanes stretch each
+    # launch); pass 2 runs one lane's share of the first batch on one lane (launches of the same
+    # shapes, each alone on the GPU).
+    roofline = None
+    prof = {}
+    if not a.no_roofline:
+        roofline, prof = profile_roofline(a, nets, groups, xs, is_vbr, elapsed / a.steps, dev)
+
+    if rank == 0:
+        images = n_jobs_total * a.steps if wl["scaling"] == "strong" else len(jobs) * world * a.steps
+        q = allrec.numpy()
+        quality = {"bpp_file_mean": round(float(q[:, F["bpp_file"]].mean()), 5),
+                   "bpp_lik_mean": round(float(q[:, F["bpp_lik"]].mean()), 5),
+                   "psnr_u8_mean": round(float(q[:, F["psnr"]].mean()), 4), "images": int(q.shape[0])}
+        if a.config in ("kodak-sweep", "vbr-mixed"):
+            per = {}
+            for lv in sorted(set(int(v) for v in q[:, F["level"]])):
+                sel = q[q[:, F["level"]] == lv]
+                key = (f"lambda_{synthetic.RATE_LAMBDAS[lv]}" if a.config == "kodak-sweep" else f"vbr_level_{lv}")
+                per[key] = {"images": int(sel.shape[0]), "bpp_file": round(float(sel[:, F["bpp_file"]].mean()), 5),
+                            "bpp_lik": round(float(sel[:, F["bpp_lik"]].mean()), 5),
+                            "psnr": round(float(sel[:, F["psnr"]].mean()), 4)}
+            quality["per_level"] = per
+        cfg0 = groups[0][0]
+        out = {
+            "metric": METRIC if a.config == "main" else f"images/sec (enc+dec), {wl['desc']}",
+            "value": round(images / elapsed, 4),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": wl["scaling"],
+            "vs_baseline": None,
+            "dtype": "f32" if a.precision == 0 else "f32 (dense convs: f32 via split-fp16 MFMA, 3 terms)",
+            "data": "synthetic (seeded sinusoid images; seeded conditioned realistic-rate weights)",
+            "config": {"workload": wl["desc"] + " (full rANS bitstreams, inputs resident in HBM)",
+                       "name": a.config, "model": wl["model"], "global_batch": n_jobs_total,
+                       "per_gpu_images": len(jobs),
+                       "shapes": sorted({f"{W}x{H}" for (_, _, H, W), _ in groups}),
+                       "weights": ("high-rate set (round 1)" if cfg0[1] is None else
+                                   f"rate set(s) {sorted({k[1] for k, _ in groups})} of synthetic.RATE_LAMBDAS"),
+                       "parallelism": f"image-sharded x{world} (no cross-GPU context)"},
+            "roofline": roofline,
+            **prof,
+            "host_thread_ms_per_step": host,
+            "host_threads": int(os.environ.get("MLIC_HOST_THREADS", "0")),
+            "wall_ms_per_step": wall_split,
+            "lanes": a.lanes,
+            "quality": quality,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            j0 = jobs[0]
+            sH, sW = (j0.H, j0.W) if j0.H * j0.W <= 1088 * 1920 else (1088, 1920)
+            out["cpu_baseline"] = cpu_baseline(j0.model, j0.rate, sH, sW, j0.level if is_vbr else -1)
+            if a.config == "kodak-sweep":
+                out["quality"]["delta_vs_cpu_oracle"] = oracle_deltas(
+                    wl["model"], sorted({k[1] for k, _ in groups}), 512, 768,
+                    {k[1]: nets[k[:2]] for k, _ in groups}, dev)
+        else:
+            out["cpu_baseline"] = None
+        if a.records_out:
+            with open(a.records_out, "w") as f:
+                json.dump({"fields": list(mdist.RECORD_FIELDS), "records": allrec.tolist()}, f)
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def profile_roofline(a, nets, groups, xs, is_vbr, t_step_s, dev):
+    from mlic_amd import _lib
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
     names = []
@@ -199,137 +414,108 @@ def main():
         _lib.call("mlic_profile_category_name", cat, nb, 128)
         names.append(nb.value.decode())
 
-    def profile_pass(lanes, xs):
-        _lib.call("mlic_set_lanes", h, lanes)
-        _lib.call("mlic_set_profiling", h, 1)
-        fam = {nm: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0} for nm in names}
-        layer_rows, phase_gpu = [], {}
+    def profile_pass(lanes, share=None):
+        fam = {}
+        layer_rows = []
+        for gi, ((model, rate, H, W), js) in enumerate(groups):
+            net = nets[(model, rate)]
+            h = net._handle
+            _lib.call("mlic_set_lanes", h, lanes)
+            _lib.call("mlic_set_profiling", h, 1)
+            x = xs[gi] if share is None else xs[gi][:share]
+            kw = {"stage": 2, "s": [j.level for j in js][:x.shape[0]]} if is_vbr else {}
 
-        def harvest(tag):
-            # per-layer table (before the reads, which clear), then per-family sums
-            n = C.c_size_t()
-            _lib.call("mlic_profile_layers", h, None, 0, C.byref(n))
-            buf = C.create_string_buffer(n.value + 1)
-            _lib.call("mlic_profile_layers", h, buf, n.value + 1, C.byref(n))
-            lines = buf.value.decode().splitlines()
-            if not layer_rows:
-                layer_rows.append("phase\t" + lines[0])
-            layer_rows.extend(f"{tag}\t{ln}" for ln in lines[1:])
-            tot = 0.0
-            for cat, nm in enumerate(names):
-                n, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
-                _lib.call("mlic_profile_read", h, cat, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
-                f = fam[nm]
-                f["launches"] += n.value
-                f["ms"] += ms.value
-                f["flops"] += fl.value
-                f["bytes"] += by.value
-                tot += ms.value
-            phase_gpu[tag] = round(tot, 3)
+            def harvest(tag):
+                n = C.c_size_t()
+                _lib.call("mlic_profile_layers", h, None, 0, C.byref(n))
+                buf = C.create_string_buffer(n.value + 1)
+                _lib.call("mlic_profile_layers", h, buf, n.value + 1, C.byref(n))
+                lines = buf.value.decode().splitlines()
+                if not layer_rows:
+                    layer_rows.append("phase\t" + lines[0])
+                layer_rows.extend(f"{tag}\t{ln}" for ln in lines[1:])
+                for cat, nm in enumerate(names):
+                    n_, ms, fl, by = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
+                    _lib.call("mlic_profile_read", h, cat, C.byref(n_), C.byref(ms), C.byref(fl), C.byref(by))
+                    if n_.value == 0:
+                        continue
+                    f = fam.setdefault(family(nm), {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+                    f["launches"] += n_.value
+                    f["ms"] += ms.value
+                    f["flops"] += fl.value
+                    f["bytes"] += by.value
 
-        c = net.compress(xs)
-        torch.cuda.synchronize()
-        harvest("compress")
-        net.decompress(c["strings"], c["shape"])
-        torch.cuda.synchronize()
-        harvest("decompress")
-        _lib.call("mlic_set_profiling", h, 0)
-        return fam, phase_gpu, layer_rows
+            c = net.compress(x, **kw)
+            torch.cuda.synchronize()
+            harvest("compress")
+            net.decompress(c["strings"], c["shape"], **kw)
+            torch.cuda.synchronize()
+            harvest("decompress")
+            _lib.call("mlic_set_profiling", h, 0)
+            _lib.call("mlic_set_lanes", h, a.lanes)
+            if share is not None:
+                break  # the isolated pass profiles one lane's share of the first batch only
+        return fam, layer_rows
 
     prof_lanes = a.profile_lanes or a.lanes
-    fam, phase_gpu, layer_rows = profile_pass(prof_lanes, x)
-    share = max(1, B // prof_lanes)
-    fam1, phase_gpu1, layer_rows1 = (profile_pass(1, x[:share]) if prof_lanes != 1
-                                     else (fam, phase_gpu, layer_rows))
-    net.set_lanes(a.lanes)
-    if a.layers_out and rank == 0:
+    fam, _ = profile_pass(prof_lanes)
+    share = max(1, groups[0][1].__len__() // prof_lanes)
+    fam1, layer_rows1 = profile_pass(1, share)
+    if a.layers_out and int(os.environ.get("RANK", "0")) == 0:
         with open(a.layers_out, "w") as f:  # isolated launches: the per-layer efficiency table
             f.write("\n".join(layer_rows1) + "\n")
 
-    def roof(fam, dom):
-        conv = fam[dom]
-        peak_tf, arith = kernel_peak(dom)
-        sec = max(conv["ms"], 1e-9) * 1e-3
-        ai = conv["flops"] / max(conv["bytes"], 1.0)
-        if ai * PEAK_HBM_GBS * 1e9 < peak_tf * 1e12:
-            return "hbm", "GB/s", conv["bytes"] / sec / 1e9, PEAK_HBM_GBS, arith, conv
-        return "mfma", "TFLOP/s", conv["flops"] / sec / 1e12, peak_tf, arith, conv
+    def bound_of(fm, name):
+        peak_tf, arith = kernel_peak(name)
+        ai = fm["flops"] / max(fm["bytes"], 1.0)
+        if fm["flops"] <= 0 or ai * PEAK_HBM_GBS * 1e9 < peak_tf * 1e12:
+            return "hbm", "GB/s", fm["bytes"] / (max(fm["ms"], 1e-9) * 1e-3) / 1e9, PEAK_HBM_GBS, arith
+        return "mfma", "TFLOP/s", fm["flops"] / (max(fm["ms"], 1e-9) * 1e-3) / 1e12, peak_tf, arith
 
-    # dominant kernel = the conv kernel family with the most device time when every launch runs alone
-    # (the isolated pass: a property of the kernels, not of how the lanes happened to interleave); its
-    # roofline bound is whichever ceiling is lower at its arithmetic intensity (algorithmic FLOPs / bytes)
-    convs = [k for k in fam if is_conv(k)]
-    dom = max(convs, key=lambda k: fam1[k]["ms"])
-    bound, unit, achieved, peak, arith, conv = roof(fam, dom)
-    _, _, achieved1, _, _, conv1 = roof(fam1, dom)
-    conv_all = {k: sum(fam[c][k] for c in convs) for k in ("launches", "ms", "flops")}
+    def t_roof_ms(fm, name):
+        peak_tf, _ = kernel_peak(name)
+        return 1e3 * max(fm["flops"] / (peak_tf * 1e12), fm["bytes"] / (PEAK_HBM_GBS * 1e9))
+
+    # dominant = the family with the most device time in the timed configuration (pass 1)
+    dom = max(fam, key=lambda k: fam[k]["ms"])
+    bound, unit, achieved, peak, arith = bound_of(fam[dom], dom)
+    iso = fam1.get(dom)
+    t_roof = sum(t_roof_ms(v, k) for k, v in fam.items())
     traffic = None
     try:
         with open(a.traffic_json) as f:
             tj = json.load(f)
-        if (tj.get("model") == a.model and tj.get("H") == H and tj.get("W") == W
-                and tj.get("family", "") and tj["family"].replace(" ", "") in dom.replace(" ", "")):
-            traffic = tj.get("conv_hbm_bytes_per_launch")
+        if tj.get("config", "main") == a.config and family(tj.get("family", "")) == dom:
+            traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
-    step_gpu_ms = sum(v["ms"] for v in fam.values())
-
-    if rank == 0:
-        images = B * world * a.steps
-        out = {
-            "metric": METRIC,
-            "value": round(images / elapsed, 4),
-            "unit": "images/sec",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1000 * elapsed / a.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32" if a.precision == 0 else "f32 (dense convs: f32 via split-fp16 MFMA, 3 terms)",
-            "data": "synthetic (seeded sinusoid images, seeded conditioned weights)",
-            "config": {"workload": f"{a.model} compress+decompress (full rANS bitstreams) of {W}x{H} images",
-                       "model": a.model, "global_batch": B * world, "per_gpu_batch": B, "H": H, "W": W,
-                       "parallelism": f"image-sharded x{world} (no cross-GPU context)"},
-            "roofline": {"bound": bound, "kernel": f"{dom} ({arith})",
-                         "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
-                         "frac": round(achieved / peak, 4),
-                         "traffic": traffic,
-                         "launches_per_step": conv["launches"],
-                         "avg_launch_us": round(1000 * conv["ms"] / max(1, conv["launches"]), 2),
-                         "algorithmic_flops_per_launch": round(conv["flops"] / max(1, conv["launches"])),
-                         "algorithmic_bytes_per_launch": round(conv["bytes"] / max(1, conv["launches"])),
-                         "all_conv_tflops": round(conv_all["flops"] / max(1e-9, conv_all["ms"] * 1e-3) / 1e12, 3),
-                         # the same kernel family, same launch shapes, every launch alone on the GPU
-                         # (one lane running one lane's share of the batch)
-                         "isolated": {"achieved": round(achieved1, 3), "frac": round(achieved1 / peak, 4),
-                                      "images": share,
-                                      "launches_per_step": conv1["launches"],
-                                      "avg_launch_us": round(1000 * conv1["ms"] / max(1, conv1["launches"]), 2)}},
-            # with profile_lanes > 1 these are per-launch durations summed over concurrently running lanes
-            "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in fam.items() if v["launches"]},
-            "gpu_kernel_ms_per_step": round(step_gpu_ms, 3),
-            "gpu_kernel_ms_by_phase": phase_gpu,
-            # one lane's share of the batch, every launch alone on the GPU (x lanes = one step's work)
-            "kernel_families_ms_isolated_share": {k: round(v["ms"], 3) for k, v in fam1.items() if v["launches"]},
-            "gpu_kernel_ms_isolated_share": round(sum(v["ms"] for v in fam1.values()), 3),
-            "isolated_share_images": share,
-            "profile_lanes": prof_lanes,
-            "host_thread_ms_per_step": host,
-            "wall_ms_per_step": wall_split,
-            "lanes": a.lanes,
-            "quality": {"bpp_file_mean": round(float(rec[:, 1].mean()), 5),
-                        "psnr_u8_mean": round(float(rec[:, 2].mean()), 4), "images": int(rec.shape[0])},
-        }
-        if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(a.model, H, W)
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
-    if distributed:
-        dist.barrier()
-        dist.destroy_process_group()
+    d = fam[dom]
+    roofline = {"bound": bound, "kernel": f"{dom} ({arith})",
+                "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / max(1, d["launches"]), 2),
+                "algorithmic_flops_per_launch": round(d["flops"] / max(1, d["launches"])),
+                "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"])),
+                "share_of_gpu_time": round(d["ms"] / max(1e-9, sum(v["ms"] for v in fam.values())), 4),
+                # T_roof = sum_k max(F_k / P_k, B_k / BW) over every kernel of one step,
+                # against the measured step time
+                "step_t_roof_ms": round(t_roof, 3), "step_ms": round(1e3 * t_step_s, 3),
+                "step_frac": round(t_roof / max(1e-9, 1e3 * t_step_s), 4)}
+    if iso:
+        _, _, ach1, _, _ = bound_of(iso, dom)
+        roofline["isolated"] = {"achieved": round(ach1, 3), "frac": round(ach1 / peak, 4), "images": share,
+                                "avg_launch_us": round(1000 * iso["ms"] / max(1, iso["launches"]), 2)}
+    prof = {
+        # with profile_lanes > 1 these are per-launch durations summed over concurrently running lanes
+        "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])},
+        "gpu_kernel_ms_per_step": round(sum(v["ms"] for v in fam.values()), 3),
+        "kernel_families_ms_isolated_share": {k: round(v["ms"], 3)
+                                              for k, v in sorted(fam1.items(), key=lambda kv: -kv[1]["ms"])},
+        "gpu_kernel_ms_isolated_share": round(sum(v["ms"] for v in fam1.values()), 3),
+        "isolated_share_images": share,
+        "profile_lanes": prof_lanes,
+    }
+    return roofline, prof
 
 
 if __name__ == "__main__":

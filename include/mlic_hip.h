@@ -41,26 +41,37 @@ int mlic_destroy(mlic_model* m);
  * outputs may be NULL.  vbr_scale = Gain[s] for *_VBR models (ignored otherwise, pass 1). */
 int mlic_forward(mlic_model* m, void* stream, const float* x, int B, int H, int W, float* x_hat, float* y_lik,
                  float* z_lik, float vbr_scale);
+/* *_v: one VBR gain per image (host array of B floats; NULL = 1), so one batch mixes levels
+ * (BASELINE config 5); equal to B calls with the scalar form, bit for bit */
+int mlic_forward_v(mlic_model* m, void* stream, const float* x, int B, int H, int W, float* x_hat, float* y_lik,
+                   float* z_lik, const float* vbr_scales);
 
 int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t* gc_len, const int32_t* gc_off,
                             int gc_n, int gc_stride, const int32_t* eb_cdf, const int32_t* eb_len,
                             const int32_t* eb_off, int eb_n, int eb_stride);
 
 /* compress/decompress split a batch over `lanes` host threads, each with its own HIP stream and
- * workspace, so the host rANS coding of one lane overlaps the kernels of another (default 2, or
+ * workspace, so the host rANS coding of one lane overlaps the kernels of another (default 4, or
  * $MLIC_LANES).  Results are identical for any lane count. */
 int mlic_set_lanes(mlic_model* m, int lanes);
 int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale);
+int mlic_compress_v(mlic_model* m, void* stream, const float* x, int B, int H, int W, const float* vbr_scales);
 int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len);
 int mlic_encoded_copy(mlic_model* m, int b, uint8_t* y, uint8_t* z);
 /* the coder inputs of image b from the last compress(): y symbols/indexes (all phases, coder order)
  * and z symbols; pass NULL buffers to query the counts */
 int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32_t* y_sym, int32_t* y_idx,
                          int32_t* z_sym);
+/* sum of -log2 of image b's y / z likelihoods in the last compress(): bpp_lik = (y + z) / (H * W) of the
+ * unpadded image (loss/rd_loss.py:42-45) */
+int mlic_encoded_bits(mlic_model* m, int b, double* y_bits, double* z_bits);
 /* y[b], z[b]: host byte strings of image b; hz, wz = latent z grid (shape returned by compress) */
 int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
                     const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
                     float vbr_scale);
+int mlic_decompress_v(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
+                      const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
+                      const float* vbr_scales);
 
 /* module-level entry points (tests / profiling): which = local|chan|inter|intra|epa|epn|lrpn|g_a|h_a|h_s|g_s|rbu|rbws */
 int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, const float* in0, const float* in1,
@@ -107,7 +118,15 @@ int mlic_local_attn_run(void* stream, int impl, const float* qkv, const float* r
 int mlic_local_attn_packed_run(void* stream, const float* qkv, const float* rel_table, const int32_t* rel_index,
                                uint16_t* out, int H, int W, int B, float scale);
 int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);
+/* per-image sum of -log2(lik) over n_per elements (fixed reduction order); synchronous */
 int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out);
+/* GaussianConditional likelihood (compressai, eval; mlicpp.py:132,168) element-wise: lik = max(Phi((0.5-|v|)/s')
+ * - Phi((-0.5-|v|)/s'), 1e-9), v = round(y - m), s' = max(s, 0.11); vbr_scale != 1 evaluates it at (y, s, m) *
+ * vbr_scale (mlicpp_vbr.py:292).  The kernel's device function is the one the slice loop runs. */
+int mlic_gaussian_likelihood(void* stream, const float* y, const float* scales, const float* means, int64_t n,
+                             float vbr_scale, float* lik);
+/* build_indexes (utils/ckbd.py:128-129): idx = (ntable-1) - #{t in table[:-1] : max(s, 0.11) <= t} */
+int mlic_scale_indexes(void* stream, const float* scales, int64_t n, const float* table, int ntable, int32_t* out);
 
 /* host entropy coder (compressai-compatible) */
 int mlic_pmf_to_quantized_cdf(const float* pmf, int n, int precision, int32_t* cdf_out /* n + 1 */);

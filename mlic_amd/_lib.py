@@ -29,6 +29,9 @@ def _sig(lib):
         "mlic_create": [C.c_char_p, i, P(C.c_char_p), P(p), P(i64), P(i), p, P(p)],
         "mlic_destroy": [p],
         "mlic_forward": [p, p, p, i, i, i, p, p, p, f],
+        "mlic_forward_v": [p, p, p, i, i, i, p, p, p, p],
+        "mlic_compress_v": [p, p, p, i, i, i, p],
+        "mlic_decompress_v": [p, p, P(p), P(sz), P(p), P(sz), i, i, i, p, p],
         "mlic_set_entropy_tables": [p, p, p, p, i, i, p, p, p, i, i],
         "mlic_compress": [p, p, p, i, i, i, f],
         "mlic_encoded_size": [p, i, P(sz), P(sz)],
@@ -53,6 +56,9 @@ def _sig(lib):
         "mlic_local_attn_packed_run": [p, p, p, p, p, i, i, i, f],
         "mlic_image_sq_err_u8": [p, p, p, i, i64, p],
         "mlic_neglog2_sum": [p, p, i, i64, p],
+        "mlic_gaussian_likelihood": [p, p, p, p, i64, f, p],
+        "mlic_scale_indexes": [p, p, i64, p, i, p],
+        "mlic_encoded_bits": [p, i, P(C.c_double), P(C.c_double)],
         "mlic_pmf_to_quantized_cdf": [p, i, i, p],
         "mlic_rans_encode": [p, p, i64, p, p, p, i, i, p, sz, P(sz)],
         "mlic_rans_decode": [p, sz, p, i64, p, p, p, i, i, p],

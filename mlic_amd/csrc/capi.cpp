@@ -83,7 +83,16 @@ int mlic_forward(mlic_model* m, void* stream, const float* x, int B, int H, int 
                  float* z_lik, float vbr_scale) {
   return guard([&] {
     MLIC_CHECK(m && x && B > 0, "bad arguments");
-    impl(m).forward(x, B, H, W, x_hat, y_lik, z_lik, vbr_scale, (hipStream_t)stream);
+    const std::vector<float> sc(B, vbr_scale);
+    impl(m).forward(x, B, H, W, x_hat, y_lik, z_lik, sc.data(), (hipStream_t)stream);
+  });
+}
+
+int mlic_forward_v(mlic_model* m, void* stream, const float* x, int B, int H, int W, float* x_hat, float* y_lik,
+                   float* z_lik, const float* vbr_scales) {
+  return guard([&] {
+    MLIC_CHECK(m && x && B > 0, "bad arguments");
+    impl(m).forward(x, B, H, W, x_hat, y_lik, z_lik, vbr_scales, (hipStream_t)stream);
   });
 }
 
@@ -100,7 +109,15 @@ int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t*
 int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale) {
   return guard([&] {
     MLIC_CHECK(m && x && B > 0, "bad arguments");
-    impl(m).compress(x, B, H, W, vbr_scale, (hipStream_t)stream);
+    const std::vector<float> sc(B, vbr_scale);
+    impl(m).compress(x, B, H, W, sc.data(), (hipStream_t)stream);
+  });
+}
+
+int mlic_compress_v(mlic_model* m, void* stream, const float* x, int B, int H, int W, const float* vbr_scales) {
+  return guard([&] {
+    MLIC_CHECK(m && x && B > 0, "bad arguments");
+    impl(m).compress(x, B, H, W, vbr_scales, (hipStream_t)stream);
   });
 }
 
@@ -132,13 +149,29 @@ int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32
   });
 }
 
+int mlic_encoded_bits(mlic_model* m, int b, double* y_bits, double* z_bits) {
+  return guard([&] {
+    const EncodedImage& e = impl(m).encoded(b);
+    if (y_bits) *y_bits = e.y_bits;
+    if (z_bits) *z_bits = e.z_bits;
+  });
+}
+
+
+int mlic_decompress_v(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
+                      const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
+                      const float* vbr_scales) {
+  return guard([&] {
+    MLIC_CHECK(m && y && z && x_hat && B > 0 && hz > 0 && wz > 0, "bad arguments");
+    impl(m).decompress(y, y_len, z, z_len, B, hz, wz, x_hat, vbr_scales, (hipStream_t)stream);
+  });
+}
+
 int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
                     const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
                     float vbr_scale) {
-  return guard([&] {
-    MLIC_CHECK(m && y && z && x_hat && B > 0 && hz > 0 && wz > 0, "bad arguments");
-    impl(m).decompress(y, y_len, z, z_len, B, hz, wz, x_hat, vbr_scale, (hipStream_t)stream);
-  });
+  const std::vector<float> sc(B > 0 ? B : 0, vbr_scale);
+  return mlic_decompress_v(m, stream, y, y_len, z, z_len, B, hz, wz, x_hat, sc.data());
 }
 
 int mlic_run_module(mlic_model* m, void* stream, const char* which, int idx, const float* in0, const float* in1,
@@ -398,8 +431,34 @@ int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, in
 
 int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out) {
   return guard([&] {
-    HIP_OK(hipMemsetAsync(out, 0, sizeof(double) * B, (hipStream_t)stream));
-    neglog2_sum(lik, n_per, B, out, (hipStream_t)stream);
+    double* part = nullptr;
+    HIP_OK(hipMalloc(&part, sizeof(double) * neglog2_partial_doubles(B)));
+    try {
+      neglog2_sum(lik, n_per, B, out, part, (hipStream_t)stream);
+      HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    } catch (...) {
+      (void)hipFree(part);
+      throw;
+    }
+    HIP_OK(hipFree(part));
+  });
+}
+
+int mlic_gaussian_likelihood(void* stream, const float* y, const float* scales, const float* means, int64_t n,
+                             float vbr_scale, float* lik) {
+  return guard([&] {
+    MLIC_CHECK(n >= 0 && (n == 0 || (y && scales && means && lik)), "gaussian_likelihood arguments");
+    gauss_likelihood(y, scales, means, n, vbr_scale, lik, (hipStream_t)stream);
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  });
+}
+
+int mlic_scale_indexes(void* stream, const float* scales, int64_t n, const float* table, int ntable, int32_t* out) {
+  return guard([&] {
+    MLIC_CHECK(ntable >= 2 && ntable <= 1024, "scale table size");
+    MLIC_CHECK(n >= 0 && (n == 0 || (scales && table && out)), "scale_indexes arguments");
+    scale_indexes(scales, n, table, ntable, out, (hipStream_t)stream);
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
   });
 }
 

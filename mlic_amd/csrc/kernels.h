@@ -138,7 +138,8 @@ struct QuantParams {
   int ntable;
   int phase;  // 0 anchor, 1 non-anchor
   int vbr;
-  float sc, rs;
+  const float* sc;  // [B] per-image VBR gain (mlicpp_vbr.py:137, Gain[s] or inputscale), when vbr
+  const float* rs;  // [B] 1 / sc, computed once on the host in fp32 (the reference's 1 / scale)
   int C, H, W, B;
 };
 void quant_phase(const QuantParams& P, hipStream_t st);
@@ -165,6 +166,12 @@ void gdn_prep(const float* beta, const float* gamma, const float* bb, const floa
 void local_mask(float* out, int H, int W, hipStream_t st);
 void sq_err_u8(const float* a, int64_t a_bs, const float* b, int64_t b_bs, double* out, int64_t n_per, int B,
                hipStream_t st);
-void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, hipStream_t st);
+// per-image sum of -log2(lik) (fixed order); part = neglog2_partial_doubles(B) doubles of scratch
+int64_t neglog2_partial_doubles(int B);
+void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, double* part, hipStream_t st);
+// GaussianConditional likelihood (vbr_scale != 1: of y*sc, s*sc, m*sc) and build_indexes, element-wise
+void gauss_likelihood(const float* y, const float* s, const float* m, int64_t n, float vbr_scale, float* lik,
+                      hipStream_t st);
+void scale_indexes(const float* s, int64_t n, const float* table, int ntable, int32_t* idx, hipStream_t st);
 
 }  // namespace mlic

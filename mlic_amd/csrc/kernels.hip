@@ -615,13 +615,14 @@ __global__ void quant_phase_kernel(QuantParams P) {
   const bool mine = (P.phase == 0) == anc;
   const float y = P.y[(int64_t)b * P.y_bs + i];
   const float* pp = P.params + (int64_t)b * P.params_bs;
+  const float sc = P.vbr ? P.sc[b] : 1.0f, rs = P.vbr ? P.rs[b] : 1.0f;
   float* yh = P.yh + (int64_t)b * P.yh_bs + i;
   if (P.lik) {
     const float* pa = P.params_a + (int64_t)b * P.params_a_bs;
     const float s = anc ? pa[(int64_t)c * HW + p] : pp[(int64_t)c * HW + p];
     const float m = anc ? pa[(int64_t)(c + P.C) * HW + p] : pp[(int64_t)(c + P.C) * HW + p];
     float lk;
-    if (P.vbr) lk = gauss_lik(y * P.sc, s * P.sc, m * P.sc);
+    if (P.vbr) lk = gauss_lik(y * sc, s * sc, m * sc);
     else lk = gauss_lik(y, s, m);
     P.lik[(int64_t)b * P.lik_bs + i] = lk;
   }
@@ -632,13 +633,13 @@ __global__ void quant_phase_kernel(QuantParams P) {
   const float s = pp[(int64_t)c * HW + p];
   const float m = pp[(int64_t)(c + P.C) * HW + p];
   float q;
-  if (P.vbr) q = rintf((y - m) * P.sc);
+  if (P.vbr) q = rintf((y - m) * sc);
   else q = rintf(y - m);
-  *yh = P.vbr ? q * P.rs + m : q + m;
+  *yh = P.vbr ? q * rs + m : q + m;
   if (P.sym) {
     const int64_t sq = (int64_t)b * P.C * HW / 2 + ((int64_t)c * P.H + h) * (P.W / 2) + (w >> 1);
     P.sym[sq] = (int32_t)q;
-    P.idx[sq] = scale_index(P.vbr ? s * P.sc : s, P.table, P.ntable);
+    P.idx[sq] = scale_index(P.vbr ? s * sc : s, P.table, P.ntable);
   }
 }
 
@@ -660,7 +661,7 @@ __global__ void phase_indexes_kernel(QuantParams P) {
   const int h = r / W2, j = r % W2;
   const int w = 2 * j + ((P.phase == 0) ? (1 - (h & 1)) : (h & 1));
   const float s = P.params[(int64_t)b * P.params_bs + (int64_t)c * HW + h * P.W + w];
-  P.idx[(int64_t)b * P.C * P.H * W2 + i] = scale_index(P.vbr ? s * P.sc : s, P.table, P.ntable);
+  P.idx[(int64_t)b * P.C * P.H * W2 + i] = scale_index(P.vbr ? s * P.sc[b] : s, P.table, P.ntable);
 }
 
 void phase_indexes(const QuantParams& P, hipStream_t st) {
@@ -686,7 +687,7 @@ __global__ void phase_dequant_kernel(QuantParams P) {
   const int64_t sq = (int64_t)b * P.C * HW / 2 + ((int64_t)c * P.H + h) * (P.W / 2) + (w >> 1);
   const float q = (float)P.sym[sq];
   const float m = P.params[(int64_t)b * P.params_bs + (int64_t)(c + P.C) * HW + p];
-  *yh = P.vbr ? q * P.rs + m : q + m;
+  *yh = P.vbr ? q * P.rs[b] + m : q + m;
 }
 
 void phase_dequant(const QuantParams& P, hipStream_t st) {
@@ -872,8 +873,11 @@ void sq_err_u8(const float* a, int64_t a_bs, const float* b, int64_t b_bs, doubl
   HIP_OK(hipGetLastError());
 }
 
-// sum of log2 likelihoods per image (bpp numerator): per-block partial sums in a fixed order
-__global__ void neglog2_sum_kernel(const float* __restrict__ lik, int64_t n_per, double* __restrict__ out) {
+// sum of -log2 likelihoods per image (the bpp numerator of loss/rd_loss.py:42-45): per-block partial
+// sums, then one fixed-order pass per image, so the result does not depend on block scheduling
+constexpr int NEGLOG2_BLOCKS = 256;
+
+__global__ void neglog2_partial_kernel(const float* __restrict__ lik, int64_t n_per, double* __restrict__ part) {
   __shared__ double red[256];
   const int img = blockIdx.y;
   double s = 0.0;
@@ -885,12 +889,54 @@ __global__ void neglog2_sum_kernel(const float* __restrict__ lik, int64_t n_per,
     if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
     __syncthreads();
   }
-  if (threadIdx.x == 0) atomicAdd(out + img, red[0]);
+  if (threadIdx.x == 0) part[(int64_t)img * NEGLOG2_BLOCKS + blockIdx.x] = red[0];
 }
 
-void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, hipStream_t st) {
-  const int nb = (int)std::min<int64_t>(256, (n_per + 255) / 256);
-  hipLaunchKernelGGL(neglog2_sum_kernel, dim3(nb, B), dim3(256), 0, st, lik, n_per, out);
+__global__ void neglog2_final_kernel(const double* __restrict__ part, int nb, double* __restrict__ out, int B) {
+  const int img = blockIdx.x * blockDim.x + threadIdx.x;
+  if (img >= B) return;
+  double s = 0.0;
+  for (int k = 0; k < nb; ++k) s += part[(int64_t)img * NEGLOG2_BLOCKS + k];
+  out[img] = s;
+}
+
+int64_t neglog2_partial_doubles(int B) { return (int64_t)B * NEGLOG2_BLOCKS; }
+
+void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, double* part, hipStream_t st) {
+  const int nb = (int)std::min<int64_t>(NEGLOG2_BLOCKS, (n_per + 255) / 256);
+  hipLaunchKernelGGL(neglog2_partial_kernel, dim3(nb, B), dim3(256), 0, st, lik, n_per, part);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(neglog2_final_kernel, dim3((B + 63) / 64), dim3(64), 0, st, part, nb, out, B);
+  HIP_OK(hipGetLastError());
+}
+
+// element-wise entry points of the slice loop's device functions (tests: A16 / A17 bit-exactness)
+__global__ void gauss_lik_kernel(const float* __restrict__ y, const float* __restrict__ s, const float* __restrict__ m,
+                                 int64_t n, float sc, int vbr, float* __restrict__ lik) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  lik[i] = vbr ? gauss_lik(y[i] * sc, s[i] * sc, m[i] * sc) : gauss_lik(y[i], s[i], m[i]);
+}
+
+void gauss_likelihood(const float* y, const float* s, const float* m, int64_t n, float vbr_scale, float* lik,
+                      hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gauss_lik_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, s, m, n, vbr_scale,
+                     vbr_scale != 1.0f ? 1 : 0, lik);
+  HIP_OK(hipGetLastError());
+}
+
+__global__ void scale_index_kernel(const float* __restrict__ s, int64_t n, const float* __restrict__ table, int nt,
+                                   int32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  idx[i] = scale_index(s[i], table, nt);
+}
+
+void scale_indexes(const float* s, int64_t n, const float* table, int ntable, int32_t* idx, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scale_index_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s, n, table, ntable,
+                     idx);
   HIP_OK(hipGetLastError());
 }
 

@@ -844,6 +844,13 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
   const int H = hyper.H, W = hyper.W, HW = H * W;
   const int64_t n_per = (int64_t)C * H * (W / 2);
   const View hyper_means = hyper.ch(hM, hM);
+  float* vbr_dev = nullptr;  // per-image VBR gains [2][B] (gain, 1 / gain)
+  if (L().vbr_on) {
+    MLIC_CHECK((int)L().vbr_host.size() == 2 * L().B, "vbr scales");
+    vbr_dev = L().arena.alloc(2 * L().B);
+    if (!L().dry)
+      HIP_OK(hipMemcpyAsync(vbr_dev, L().vbr_host.data(), sizeof(float) * 2 * L().B, hipMemcpyHostToDevice, L().st));
+  }
   for (int idx = 0; idx < S; ++idx) {
     const size_t m = L().arena.mark();
     View ysl = yhat.ch(idx * C, C);
@@ -867,8 +874,8 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       Q.table = scale_table_;
       Q.ntable = 64;
       Q.vbr = L().vbr_on ? 1 : 0;
-      Q.sc = L().vbr_sc;
-      Q.rs = L().vbr_rs;
+      Q.sc = vbr_dev;
+      Q.rs = vbr_dev + L().B;
       Q.phase = ph;
       View pn;
       if (ph == 1) {
@@ -897,7 +904,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       } else {
         Q.y = y->p + (int64_t)idx * C * HW;
         Q.y_bs = y->bs;
-        if (ph == 1 && mode == Mode::Forward && y_lik) {
+        if (ph == 1 && mode != Mode::Decode && y_lik) {
           Q.lik = y_lik + (int64_t)idx * C * HW;
           Q.lik_bs = (int64_t)cfg_.M * HW;
           Q.params_a = pa.p;
@@ -962,11 +969,17 @@ void Model::ensure_host(size_t n) {
   l.h_cap = n;
 }
 
-void Model::set_vbr(float scale) {
+void Model::set_vbr(const float* scales, int B) {
   Lane& l = L();
   l.vbr_on = cfg_.vbr;
-  l.vbr_sc = scale;
-  l.vbr_rs = 1.0f / scale;
+  l.vbr_host.assign(2 * B, 1.0f);
+  if (!l.vbr_on) return;
+  for (int b = 0; b < B; ++b) {
+    const float s = scales ? scales[b] : 1.0f;
+    MLIC_CHECK(std::isfinite(s) && s > 0.0f, "VBR gain must be finite and positive");
+    l.vbr_host[b] = s;
+    l.vbr_host[B + b] = 1.0f / s;  // mlicpp_vbr.py: rescale by 1 / scale
+  }
 }
 
 hipEvent_t Model::next_event() {
@@ -1098,7 +1111,7 @@ void Model::over_lanes(int B, hipStream_t caller, F&& fn) {
 }
 
 // ------------------------------------------------------------------------------------- entry points
-void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
+void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, const float* vbr_scales,
                     hipStream_t st) {
   MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64 (pad like utils/testing.py:130-137)");
   // forward() runs on the caller's stream in lane 0 (torch-ordered, capturable)
@@ -1111,7 +1124,7 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
     ~Restore() { l.st = s; tl_lane_ = nullptr; }
   } restore{l, own};
   l.st = st;  // caller's stream, including the legacy NULL stream torch uses by default
-  set_vbr(vbr_scale);
+  set_vbr(vbr_scales, B);
   planned(B, st, [&] {
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
@@ -1128,13 +1141,13 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
   });
 }
 
-void Model::compress(const float* x, int B, int H, int W, float vbr_scale, hipStream_t st) {
+void Model::compress(const float* x, int B, int H, int W, const float* vbr_scales, hipStream_t st) {
   MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64");
   MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
   enc_all_.assign(B, EncodedImage{});
   const int64_t img = (int64_t)3 * H * W;
   over_lanes(B, st, [&](Lane& l, int first, int cnt) {
-    set_vbr(vbr_scale);
+    set_vbr(vbr_scales ? vbr_scales + first : nullptr, cnt);
     compress_lane(x + first * img, cnt, H, W);
     for (int b = 0; b < cnt; ++b) enc_all_[first + b] = std::move(l.enc[b]);
   });
@@ -1149,19 +1162,31 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   const int nph = 2 * cfg_.S;
   const int64_t ny = (int64_t)nph * B * n_per, nz = (int64_t)B * cfg_.N * hz * wz;
   int32_t *d_sym = nullptr, *d_idx = nullptr, *d_zsym = nullptr;
+  double* d_bits = nullptr;  // [2][B]: -log2 likelihood sums of y and z per image (B1, rd_loss.py:42-45)
   planned(B, nullptr, [&] {
     d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
     d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
     d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(nz));
+    d_bits = reinterpret_cast<double*>(l.arena.alloc(4 * B));
+    double* part = reinterpret_cast<double*>(l.arena.alloc(4 * neglog2_partial_doubles(B)));
+    const int64_t ny_img = (int64_t)cfg_.M * h * w, nz_img = (int64_t)cfg_.N * hz * wz;
+    float* y_lik = l.arena.alloc(B * ny_img);
+    float* z_lik = l.arena.alloc(B * nz_img);
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
     View z = h_a(y);
     View zh = alloc(z.C, z.H, z.W);
-    eb(z, zh, nullptr, d_zsym);  // z_hat = round(z - med) + med == decompress(compress(z))
+    eb(z, zh, z_lik, d_zsym);  // z_hat = round(z - med) + med == decompress(compress(z))
     View hyper = h_s(zh);
     View yhat = alloc(cfg_.M, y.H, y.W);
-    slice_loop(Mode::Encode, hyper, &y, yhat, nullptr, d_sym, d_idx, nullptr);
+    slice_loop(Mode::Encode, hyper, &y, yhat, y_lik, d_sym, d_idx, nullptr);
+    timed(PCAT_ELEM, 0.0, 4.0 * B * (ny_img + nz_img), [&] {
+      neglog2_sum(y_lik, ny_img, B, d_bits, part, l.st);
+      neglog2_sum(z_lik, nz_img, B, d_bits + B, part + neglog2_partial_doubles(B), l.st);
+    }, "bpp_lik");
   });
+  std::vector<double> bits(2 * B);
+  HIP_OK(hipMemcpyAsync(bits.data(), d_bits, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, l.st));
   ensure_host((size_t)(ny + nz));
   int32_t* hs = l.h_sym;
   int32_t* hi = l.h_idx;
@@ -1174,6 +1199,10 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     HIP_OK(hipStreamSynchronize(l.st));
   }
   l.enc.assign(B, EncodedImage{});
+  for (int b = 0; b < B; ++b) {
+    l.enc[b].y_bits = bits[b];
+    l.enc[b].z_bits = bits[B + b];
+  }
   const int64_t zper = (int64_t)cfg_.N * hz * wz;
   auto work = [&](int b) {
     HostStats::Scope e{hstats_.enc_ns};
@@ -1195,22 +1224,26 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   host_pool().run(B, work);
 }
 
+// one process-wide pool (every handle's lanes submit to it): a sweep over several weight sets does
+// not multiply the coder threads; $MLIC_HOST_THREADS (bench.py sets cores / ranks-per-node)
 HostPool& Model::host_pool() {
-  std::call_once(pool_once_, [this] {
+  static std::once_flag once;
+  static std::unique_ptr<HostPool> pool;
+  std::call_once(once, [] {
     int n = (int)std::thread::hardware_concurrency();
     if (const char* e = std::getenv("MLIC_HOST_THREADS")) n = std::atoi(e);
     n = std::max(1, std::min(n, 16));
-    pool_ = std::make_unique<HostPool>(n);
+    pool = std::make_unique<HostPool>(n);
   });
-  return *pool_;
+  return *pool;
 }
 
 void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
-                       int B, int hz, int wz, float* x_hat, float vbr_scale, hipStream_t st) {
+                       int B, int hz, int wz, float* x_hat, const float* vbr_scales, hipStream_t st) {
   MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
   const int64_t img = (int64_t)3 * 64 * hz * 64 * wz;
   over_lanes(B, st, [&](Lane& l, int first, int cnt) {
-    set_vbr(vbr_scale);
+    set_vbr(vbr_scales ? vbr_scales + first : nullptr, cnt);
     decompress_lane(y + first, ylen + first, z + first, zlen + first, cnt, hz, wz, x_hat + first * img);
   });
 }

@@ -72,6 +72,7 @@ struct EncodedImage {
   std::string y;  // one rANS stream for all slices/phases
   std::string z;  // z stream (EntropyBottleneck)
   std::vector<int32_t> y_sym, y_idx, z_sym;  // the coder inputs, in coder order (tests / tooling)
+  double y_bits = 0, z_bits = 0;  // sum of -log2 of the y / z likelihoods (rd_loss.py:42-45 numerator)
 };
 
 class PhaseDecoder;
@@ -97,7 +98,7 @@ struct Lane {
   bool own_stream = false;
   int B = 0;
   bool dry = false;
-  float vbr_sc = 1.0f, vbr_rs = 1.0f;
+  std::vector<float> vbr_host;  // [2][B]: per-image gain, then 1 / gain (uploaded by slice_loop)
   bool vbr_on = false;
   std::vector<EncodedImage> enc;
   int32_t* h_sym = nullptr;
@@ -127,14 +128,15 @@ class Model {
   HostPool& host_pool();  // shared entropy-coding workers ($MLIC_HOST_THREADS, <= 16)
 
   // forward(): x [B,3,H,W] -> x_hat, y_lik [B,M,H/16,W/16], z_lik [B,N,H/64,W/64] (any may be null)
-  void forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, float vbr_scale,
+  // vbr_scales: per-image Gain (host array of B; null = 1 for all); only *_VBR models use it
+  void forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, const float* vbr_scales,
                hipStream_t st);
   // compress(): network + rANS; results readable with encoded(b)
-  void compress(const float* x, int B, int H, int W, float vbr_scale, hipStream_t st);
+  void compress(const float* x, int B, int H, int W, const float* vbr_scales, hipStream_t st);
   const EncodedImage& encoded(int b) const { return enc_all_.at(b); }
   // decompress(): y/z byte streams per image -> x_hat [B,3,4*16*hz,4*16*wz]
   void decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen, int B,
-                  int hz, int wz, float* x_hat, float vbr_scale, hipStream_t st);
+                  int hz, int wz, float* x_hat, const float* vbr_scales, hipStream_t st);
   void set_tables(const CdfTables& gc, const CdfTables& eb) {
     gc_ = gc;
     eb_ = eb;
@@ -165,11 +167,9 @@ class Model {
   CdfTables gc_, eb_;
   std::vector<EncodedImage> enc_all_;
   std::vector<std::unique_ptr<Lane>> lanes_;
-  int nlanes_ = 2;
+  int nlanes_ = 4;
   int precision_ = PREC_F16X3_V2;
   HostStats hstats_;
-  std::once_flag pool_once_;
-  std::unique_ptr<HostPool> pool_;
   bool prof_ = false;
   static thread_local Lane* tl_lane_;
   Lane& L() const { return *tl_lane_; }
@@ -226,7 +226,7 @@ class Model {
   template <class F>
   void planned(int B, hipStream_t st, F&& body);
   void ensure_host(size_t n);
-  void set_vbr(float scale);
+  void set_vbr(const float* scales, int B);
 };
 
 }  // namespace mlic

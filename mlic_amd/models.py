@@ -151,8 +151,9 @@ class MLICPlusPlus(nn.Module):
             _lib.call("mlic_set_precision", h, self._precision)
         return h
 
-    def _vbr_scale(self, **kw) -> float:
-        return 1.0
+    def _vbr_scales(self, B: int, **kw) -> np.ndarray:
+        """Per-image VBR gain (float32 [B]); 1 for fixed-rate models."""
+        return np.ones(B, np.float32)
 
     def set_precision(self, mode: int):
         """Dense-conv arithmetic: 1 = split-fp16 MFMA "f16x3" (default), 0 = fp32 MFMA."""
@@ -189,8 +190,9 @@ class MLICPlusPlus(nn.Module):
         x_hat = torch.empty_like(x)
         y_lik = torch.empty(B, self.M, H // 16, W // 16, device=x.device)
         z_lik = torch.empty(B, self.N, H // 64, W // 64, device=x.device)
-        _lib.call("mlic_forward", h, self._stream(), x.data_ptr(), B, H, W, x_hat.data_ptr(), y_lik.data_ptr(),
-                  z_lik.data_ptr(), C.c_float(self._vbr_scale(**kw)))
+        sc = self._vbr_scales(B, **kw)
+        _lib.call("mlic_forward_v", h, self._stream(), x.data_ptr(), B, H, W, x_hat.data_ptr(), y_lik.data_ptr(),
+                  z_lik.data_ptr(), sc.ctypes.data)
         return {"x_hat": x_hat, "likelihoods": {"y_likelihoods": y_lik, "z_likelihoods": z_lik}}
 
     def update(self, scale_table=None, force: bool = False) -> bool:
@@ -250,7 +252,8 @@ class MLICPlusPlus(nn.Module):
         h = self._ensure_handle(x.device)
         self._push_tables(h)
         x = x.contiguous().float()
-        _lib.call("mlic_compress", h, self._stream(), x.data_ptr(), B, H, W, C.c_float(self._vbr_scale(**kw)))
+        sc = self._vbr_scales(B, **kw)
+        _lib.call("mlic_compress_v", h, self._stream(), x.data_ptr(), B, H, W, sc.ctypes.data)
         ys, zs = [], []
         for b in range(B):
             yl, zl = C.c_size_t(), C.c_size_t()
@@ -283,8 +286,9 @@ class MLICPlusPlus(nn.Module):
         zp = (C.c_void_p * B)(*[C.cast(b, C.c_void_p) for b in zbufs])
         yl = (C.c_size_t * B)(*[len(s) for s in ys])
         zl = (C.c_size_t * B)(*[len(s) for s in zs])
-        _lib.call("mlic_decompress", h, self._stream(), yp, yl, zp, zl, B, hz, wz, x_hat.data_ptr(),
-                  C.c_float(self._vbr_scale(**kw)))
+        sc = self._vbr_scales(B, **kw)
+        _lib.call("mlic_decompress_v", h, self._stream(), yp, yl, zp, zl, B, hz, wz, x_hat.data_ptr(),
+                  sc.ctypes.data)
         torch.cuda.synchronize(dev)
         return {"x_hat": x_hat, "cost_time": time.time() - t0}
 
@@ -297,6 +301,13 @@ class MLICPlusPlus(nn.Module):
         _lib.call("mlic_encoded_streams", self._handle, b, C.byref(ny), C.byref(nz), ys.ctypes.data,
                   yi.ctypes.data, zs.ctypes.data)
         return ys, yi, zs
+
+    def likelihood_bits(self, b: int = 0):
+        """(y_bits, z_bits): sum of -log2 of image b's y / z likelihoods in the last compress(),
+        computed on the device; bpp_lik = (y_bits + z_bits) / (H * W) (loss/rd_loss.py:42-45)."""
+        yb, zb = C.c_double(), C.c_double()
+        _lib.call("mlic_encoded_bits", self._handle, b, C.byref(yb), C.byref(zb))
+        return yb.value, zb.value
 
     def aux_loss(self):
         """compressai EntropyBottleneck.loss(): |logits_cumulative(quantiles) - target| (training aid)."""
@@ -333,22 +344,32 @@ class MLICPlusPlusVbr(MLICPlusPlus):
         self.lmbda = list(spec.VBR_LAMBDAS)
         self.levels = len(self.lmbda)
 
-    def _vbr_scale(self, stage: int = 2, s: int = 1, inputscale=0, **kw) -> float:
+    def _vbr_scales(self, B: int, stage: int = 2, s=1, inputscale=0, **kw) -> np.ndarray:
+        """mlicpp_vbr.py:122-137: scale = inputscale if given, else Gain[s] (clamped to the levels).
+        `s` / `inputscale` may be one value for the batch or one per image (BASELINE config 5)."""
         if stage != 2:
             raise ValueError("only the inference stage (stage=2) is supported")
-        if inputscale:
-            return float(inputscale)
-        g = self.Gain.detach().float().cpu()
-        s = max(0, min(int(s), len(g) - 1))
-        return float(g[s])
+        g = self.Gain.detach().float().cpu().numpy()
 
-    def forward(self, x, stage: int = 2, s: int = 1, inputscale=0):
+        def per_image(v):
+            a = np.asarray(v.detach().cpu() if torch.is_tensor(v) else v).reshape(-1)
+            if a.size == 1:
+                return np.repeat(a, B)
+            if a.size != B:
+                raise ValueError(f"expected 1 or {B} per-image values, got {a.size}")
+            return a
+        ins = per_image(inputscale).astype(np.float64)
+        lv = np.clip(per_image(s).astype(np.int64), 0, len(g) - 1)
+        out = np.where(ins != 0, ins, g[lv]).astype(np.float32)
+        return np.ascontiguousarray(out)
+
+    def forward(self, x, stage: int = 2, s=1, inputscale=0):
         return super().forward(x, stage=stage, s=s, inputscale=inputscale)
 
-    def compress(self, x, stage: int = 2, s: int = 1, inputscale=0):
+    def compress(self, x, stage: int = 2, s=1, inputscale=0):
         return super().compress(x, stage=stage, s=s, inputscale=inputscale)
 
-    def decompress(self, strings, shape, stage: int = 2, s: int = 1, inputscale=0):
+    def decompress(self, strings, shape, stage: int = 2, s=1, inputscale=0):
         return super().decompress(strings, shape, stage=stage, s=s, inputscale=inputscale)
 
 

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import math
 import zlib
-from typing import Dict
+from typing import Dict, Optional
 
 import numpy as np
 import torch
@@ -125,9 +125,60 @@ def relative_position_index(window: int) -> np.ndarray:
     return (dh * (2 * window - 1) + dw).astype(np.int64)
 
 
-def synth_state_dict(name: str, seed: int = 0) -> Dict[str, torch.Tensor]:
-    """Conditioned synthetic state_dict for model `name` (CPU tensors)."""
+# Realistic-rate weight sets: stand-ins for the six lambda checkpoints of README.md:109-114
+# (lambda 0.0018 ... 0.0483; the checkpoints are not reachable offline and are shape-incompatible
+# with this fork).  All levels share one draw (seed 100) and differ by one rate knob t, so the six
+# sets are ordered by rate like an RD curve: y gain (1 + t) / 24 of the default set, EP scale bias
+# -2.5 + t, scale-weight gain (1 + t) / 40, a sharper factorized z prior (compressai init_scale 1,
+# quantiles med +- 3).  CPU oracle, MLICPP_L, 256x384: bpp 0.135 / 0.171 / 0.233 / 0.331 / 0.477 /
+# 0.672 (z ~0.11 of it) -- the spread of the reference's Kodak RD points
+# (results/kodak/mlicplusplus_mse.json:2-17).  The synthetic decoder is not trained, so PSNR stays ~14 dB.
+RATE_LAMBDAS = (0.0018, 0.0035, 0.0067, 0.0130, 0.0250, 0.0483)
+_RATE_T = (0.0, 0.15, 0.3, 0.45, 0.6, 0.75)
+
+
+def rate_seed(level: int) -> int:
+    return 100
+
+
+def _apply_rate(out: Dict[str, torch.Tensor], cfg: spec.ModelConfig, level: int) -> None:
+    t = _RATE_T[level]
+    for key in list(out):
+        a = out[key]
+        if key.endswith(("g_a.analysis_transform.6.point_conv.weight", "g_a.analysis_transform.6.weight")):
+            out[key] = a * ((1.0 + t) / 24.0)
+        elif key.endswith(("h_a.reduction.8.point_conv.weight", "h_a.reduction.8.weight")):
+            out[key] = a * (4.0 / 40.0)
+        elif key.startswith("entropy_parameters") and key.endswith(".fusion.6.bias"):
+            a = a.clone()
+            a[: cfg.slice_ch] += (-2.5 + t) - 1.2
+            out[key] = a
+        elif key.startswith("entropy_parameters") and key.endswith(".fusion.6.weight"):
+            a = a.clone()
+            a[: cfg.slice_ch] *= (1.0 + t) / 40.0
+            out[key] = a
+    f = (1, 3, 3, 3, 3, 1)
+    old_sc, new_sc = 10.0 ** (1 / 5), 1.0
+    for i in range(5):
+        k = f"entropy_bottleneck._matrix{i}"
+        if k in out:
+            shift = math.log(math.expm1(1 / new_sc / f[i + 1])) - math.log(math.expm1(1 / old_sc / f[i + 1]))
+            out[k] = out[k] + shift
+    q = out.get("entropy_bottleneck.quantiles")
+    if q is not None:
+        med = q[:, 0, 1]
+        out["entropy_bottleneck.quantiles"] = torch.stack([med - 3.0, med, med + 3.0], -1).reshape(q.shape).contiguous()
+
+
+def synth_state_dict(name: str, seed: int = 0, rate: Optional[int] = None) -> Dict[str, torch.Tensor]:
+    """Conditioned synthetic state_dict for model `name` (CPU tensors).  rate=None: the default
+    high-rate set (~10 bpp); rate=r in 0..5: the realistic-rate set r (seed 100, see RATE_LAMBDAS),
+    in which case `seed` is ignored."""
     cfg = spec.get_config(name)
+    if rate is not None:
+        if not 0 <= int(rate) < len(_RATE_T):
+            raise ValueError(f"rate level must be in 0..{len(_RATE_T) - 1}")
+        seed = rate_seed(rate)
     out: Dict[str, torch.Tensor] = {}
     for key, shape in spec.state_dict_shapes(name).items():
         a = _draw(key, shape, cfg, seed)
@@ -144,6 +195,10 @@ def synth_state_dict(name: str, seed: int = 0) -> Dict[str, torch.Tensor]:
             a = a.copy()
             a[: cfg.slice_ch] *= 40.0
         out[key] = torch.from_numpy(np.ascontiguousarray(a))
+    if rate is not None:
+        _apply_rate(out, cfg, int(rate))
+        for k in out:
+            out[k] = out[k].contiguous()
     return out
 
 

@@ -76,9 +76,9 @@ def gen_bitexact():
          cdf_length=gc.cdf_length, sweep=sweep, sweep_indexes=gc.build_indexes(sweep))
 
 
-def _ref_model(name, seed):
+def _ref_model(name, seed, rate=None):
     m = refload.build(name)
-    sd = synthetic.synth_state_dict(name, seed)
+    sd = synthetic.synth_state_dict(name, seed, rate=rate)
     m.load_state_dict(sd)
     return m.eval(), sd
 
@@ -135,8 +135,8 @@ def gen_modules():
          sd_sha=sd_checksum(sd))
 
 
-def gen_forward(name, H, W, seed=0, img_seed=0, s=None, with_streams=False):
-    m, sd = _ref_model(name, seed)
+def gen_forward(name, H, W, seed=0, img_seed=0, s=None, with_streams=False, rate=None):
+    m, sd = _ref_model(name, seed, rate)
     x = synthetic.synth_image(H, W, img_seed)
     with torch.no_grad():
         out = m(x) if s is None else m(x, stage=2, s=s)
@@ -161,14 +161,14 @@ def gen_forward(name, H, W, seed=0, img_seed=0, s=None, with_streams=False):
         arr["y_indexes"] = np.asarray(captured["idx"], np.int32)
         arr["z_symbols"] = torch.stack([s_[1] for s_ in c["strings"][1]])
         arr["z_shape"] = np.asarray(list(c["shape"]), np.int32)
-    tag = f"{name}_{H}x{W}" + ("" if s is None else f"_s{s}")
+    tag = f"{name}_{H}x{W}" + ("" if s is None else f"_s{s}") + ("" if rate is None else f"_r{rate}")
     save(f"forward_{tag}.npz", **arr)
     print(f"  {tag}: bpp={bpp:.4f}")
 
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    what = sys.argv[1:] or ["bitexact", "modules", "forward"]
+    what = sys.argv[1:] or ["bitexact", "modules", "forward", "rates"]
     if "bitexact" in what:
         gen_bitexact()
     if "modules" in what:
@@ -182,6 +182,13 @@ def main():
         gen_forward("MLICPP_M_SMALL_DEC", 128, 128, with_streams=True)
         for s in (0, 3, 5):
             gen_forward("MLICPP_L_VBR", 128, 128, s=s)
+    if "rates" in what:
+        # realistic-rate weight sets (synthetic.RATE_LAMBDAS stand-ins): 0.1-0.7 bpp, coder streams
+        for r in (0, 2, 5):
+            gen_forward("MLICPP_L", 192, 256, img_seed=3, rate=r, with_streams=True)
+        gen_forward("MLICPP_S", 192, 256, img_seed=3, rate=1, with_streams=True)
+        gen_forward("MLICPP_M_SMALL_DEC", 192, 256, img_seed=3, rate=1, with_streams=True)
+        gen_forward("MLICPP_L_VBR", 192, 256, img_seed=3, rate=2, s=1)
 
 
 if __name__ == "__main__":

@@ -60,3 +60,53 @@ def test_gather_records_world2():
     assert tmax == 2.0
     assert [int(r[0]) for r in rows] == list(range(njobs))
     assert all(abs(r[8] - (30.0 + r[0])) < 1e-9 for r in rows)
+
+
+def _sweep_worker(rank, world, port, q):
+    import argparse
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a = argparse.Namespace(config="kodak-sweep", rate=1, batch=0)
+    jobs, total = bench.build_jobs(a, rank, world)
+    F = {k: i for i, k in enumerate(mdist.RECORD_FIELDS)}
+    rec = torch.zeros(len(jobs), mdist.RECORD_LEN, dtype=torch.float64)
+    for k, j in enumerate(jobs):
+        rec[k, F["job"]], rec[k, F["H"]], rec[k, F["W"]], rec[k, F["level"]] = j.id, j.H, j.W, j.level
+        rec[k, F["bpp_lik"]] = 0.1 * (1 + j.level)
+        rec[k, F["psnr"]] = 30.0 + j.id
+    mx = torch.tensor([len(jobs)])
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    allrec = mdist.gather_records(rec, max_per_rank=int(mx))
+    n_batches = len(bench.batches(jobs))
+    if rank == 0:
+        q.put((allrec.tolist(), total, [len(jobs)], n_batches))
+    else:
+        q.put((None, total, [len(jobs)], n_batches))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_kodak_sweep_sharded_world2():
+    """BASELINE config 4's job list (24 Kodak-size images incl. 4 portrait x 6 lambda stand-ins = 144
+    jobs) sharded by bench.py over 2 ranks with LPT; the gathered records are complete and sorted."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sweep_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rows = next(g[0] for g in got if g[0] is not None)
+    assert all(g[1] == 144 for g in got)
+    counts = sorted(g[2][0] for g in got)
+    assert sum(counts) == 144 and counts[1] - counts[0] <= 4  # LPT by pixels: balanced to one job's worth
+    assert [int(r[0]) for r in rows] == list(range(144))
+    for r in rows:
+        j = int(r[0])
+        assert int(r[3]) == j // 24  # lambda level
+        assert (int(r[1]), int(r[2])) == ((512, 768) if j % 24 < 20 else (768, 512))

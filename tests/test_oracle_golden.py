@@ -119,3 +119,32 @@ def test_compress_streams_match_reference(golden, name, H, W):
     dec = m.decode_streams(st["z_symbols"], [p[0] for p in st["phases"]])
     assert torch.equal(dec["y_hat"], st["y_hat"])
     close(dec["x_hat"], g["x_hat"], rtol=1e-4, atol=1e-4)
+
+
+# realistic-rate weight sets (synthetic.RATE_LAMBDAS stand-ins, 0.06-0.9 bpp): forward and the exact
+# coder inputs, oracle vs the reference (oracle/gen_golden.py "rates")
+RATES = [("MLICPP_L", 0, None), ("MLICPP_L", 2, None), ("MLICPP_L", 5, None), ("MLICPP_S", 1, None),
+         ("MLICPP_M_SMALL_DEC", 1, None), ("MLICPP_L_VBR", 2, 1)]
+
+
+@pytest.mark.parametrize("name,rate,s", RATES)
+def test_rate_sets_match_reference(golden, name, rate, s):
+    H, W = 192, 256
+    tag = f"{name}_{H}x{W}" + ("" if s is None else f"_s{s}") + f"_r{rate}"
+    g = golden(f"forward_{tag}.npz")
+    sd = synthetic.synth_state_dict(name, rate=rate)
+    assert sd_sha(sd) == str(g["sd_sha"]), "synthetic weights drifted from the fixture"
+    x = synthetic.synth_image(H, W, 3)
+    assert hashlib.sha256(x.numpy().tobytes()).hexdigest() == str(g["x_sha"])
+    m = ref.RefMLIC(name, sd)
+    out = m.forward(x, s=1 if s is None else s)
+    yl, zl = out["likelihoods"]["y_likelihoods"], out["likelihoods"]["z_likelihoods"]
+    assert abs(ref.bpp_from_likelihoods(yl, zl, H * W) - float(g["bpp"])) < 1e-4
+    close(out["x_hat"], g["x_hat"], rtol=1e-4, atol=1e-4)
+    if "y_symbols" in g.files:
+        st = m.compress_streams(x)
+        sym = torch.cat([p[0].reshape(-1) for p in st["phases"]]).numpy()
+        idx = torch.cat([p[1].reshape(-1) for p in st["phases"]]).numpy()
+        assert np.array_equal(st["z_symbols"].numpy(), g["z_symbols"])
+        assert np.array_equal(idx, g["y_indexes"])
+        assert np.array_equal(sym, g["y_symbols"])
