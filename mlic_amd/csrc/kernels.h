@@ -73,7 +73,8 @@ enum ProfCat : int {
   PCAT_LINATT = 18,
   PCAT_ELEM = 19,
   PCAT_CONV_X4 = 20,
-  PCAT_COUNT = 21
+  PCAT_CHAIN = 21,
+  PCAT_COUNT = 22
 };
 int conv_prof_cat(int impl, const ConvParams& P);
 const char* prof_cat_name(int cat);
@@ -173,5 +174,25 @@ void neglog2_sum(const float* lik, int64_t n_per, int B, double* out, double* pa
 void gauss_likelihood(const float* y, const float* s, const float* m, int64_t n, float vbr_scale, float* lik,
                       hipStream_t st);
 void scale_indexes(const float* s, int64_t n, const float* table, int ntable, int32_t* idx, hipStream_t st);
+
+// fused 1x1 chain (chain.hip): layer widths cout[0..nl-1] in {320,256,128,64|128} (EntropyParameters)
+// or {128,64} (LocalContext MLP); weights pre-packed by chain_pack per layer, concatenated
+struct ChainParams {
+  Seg seg[MAXSEG];
+  int nseg, cin0;  // layer-0 input: channel concat, cin0 % 32 == 0
+  int HW, B;       // pixels per image (HW % 4 == 0)
+  const float* bias[4];
+  int gelu_mask;   // bit l: GELU after layer l (l < nl - 1)
+  const _Float16* wimg;
+  float* out;      // [B][cout[nl-1]][HW] (batch stride out_bs)
+  int64_t out_bs;
+  const float* res;  // optional residual added to the output (same layout, batch stride res_bs)
+  int64_t res_bs;
+};
+bool chain_supported(int nl, const int* cout);
+int64_t chain_layer_halves(int Cout, int Cin);
+void chain_pack(const _Float16* wh, const _Float16* wl, int Cout, int Cin, int cin_pad, int permute, _Float16* dst,
+                hipStream_t st);
+void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st);
 
 }  // namespace mlic

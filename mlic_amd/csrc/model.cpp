@@ -208,6 +208,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     rel_index_ = reinterpret_cast<int*>(take(ww * ww));
     HIP_OK(hipMemcpyAsync(rel_index_, ri.data(), ri.size() * 4, hipMemcpyHostToDevice, st));
   }
+  add_chains(st);
   MLIC_CHECK(raw_.count("__scale_table"), "scale table missing");
   scale_table_ = const_cast<float*>(raw_["__scale_table"]);
   HIP_OK(hipStreamSynchronize(st));
@@ -248,6 +249,67 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
   cw.wx4 = wx;
   cw.name = base;
   convs_[base + ".__x4perm"] = cw;
+}
+
+// LDS weight images of the fused chains: EntropyParameters (entropy.py:10-18, layers .0 .2 .4 .6) and
+// LocalContext's MLP (context.py:108-110, fc1 fc2)
+void Model::add_chains(hipStream_t st) {
+  std::vector<std::pair<std::string, std::vector<std::string>>> todo;
+  for (auto& kv : convs_) {
+    const std::string& k = kv.first;
+    if (k.rfind("entropy_parameters", 0) == 0 && ends_with(k, ".fusion.0")) {
+      const std::string p = k.substr(0, k.size() - 2);
+      todo.push_back({p, {p + ".0", p + ".2", p + ".4", p + ".6"}});
+    } else if (k.rfind("local_context", 0) == 0 && ends_with(k, ".mlp.fc1")) {
+      const std::string p = k.substr(0, k.size() - 4);
+      todo.push_back({p, {p + ".fc1", p + ".fc2"}});
+    }
+  }
+  int64_t total = 0;
+  std::vector<ChainW> cws;
+  for (auto& t : todo) {
+    ChainW c;
+    c.name = t.first;
+    c.nl = (int)t.second.size();
+    bool ok = true;
+    for (int l = 0; l < c.nl; ++l) {
+      auto it = convs_.find(t.second[l]);
+      if (it == convs_.end() || it->second.K != 1 || !it->second.wh) { ok = false; break; }
+      const ConvW& w = it->second;
+      c.cout[l] = w.Cout;
+      c.bias[l] = w.b;
+      if (l == 0) c.cin0 = w.Cin;
+      else if (w.Cin != c.cout[l - 1]) ok = false;
+      total += chain_layer_halves(w.Cout, w.Cin);
+    }
+    if (ok && chain_supported(c.nl, c.cout) && c.cin0 % 32 == 0) cws.push_back(c);
+  }
+  if (cws.empty()) return;
+  _Float16* blk = nullptr;
+  HIP_OK(hipMalloc(&blk, (size_t)total * sizeof(_Float16)));
+  owned_.push_back(blk);
+  wbytes_ += (size_t)total * sizeof(_Float16);
+  int64_t off = 0;
+  for (ChainW& c : cws) {
+    c.wimg = blk + off;
+    const auto& names = c.nl == 4 ? std::vector<std::string>{c.name + ".0", c.name + ".2", c.name + ".4", c.name + ".6"}
+                                  : std::vector<std::string>{c.name + ".fc1", c.name + ".fc2"};
+    for (int l = 0; l < c.nl; ++l) {
+      const ConvW& w = convs_.at(names[l]);
+      chain_pack(w.wh, w.wl, w.Cout, w.Cin, w.cin_pad, l > 0 ? 1 : 0, blk + off, st);
+      off += chain_layer_halves(w.Cout, w.Cin);
+    }
+    chains_[c.name] = c;
+  }
+}
+
+// $MLIC_CHAIN=0: the per-layer path for EntropyParameters / LocalContext MLP (A/B switch)
+bool Model::chain_on() const {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_CHAIN");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && precision_ == PREC_F16X3_V2;
 }
 
 Model::~Model() {
@@ -448,6 +510,39 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
   P.B = L().B;
   const double outn = (double)L().B * c * P.Ho * P.Wo;
   timed(PCAT_DW, 18.0 * outn, 4.0 * ((double)L().B * c * P.H * P.W + outn), [&] { dw3x3(P, L().st); }, w.name);
+}
+
+// a fused chain over a (multi-segment) input; GELU between the layers (entropy.py:10-18, MLP fc1 -> fc2)
+void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res) {
+  ChainParams P{};
+  MLIC_CHECK(!ins.empty() && (int)ins.size() <= MAXSEG, "chain inputs");
+  P.nseg = (int)ins.size();
+  int cin = 0;
+  for (int s = 0; s < P.nseg; ++s) {
+    MLIC_CHECK(ins[s].H == ins[0].H && ins[s].W == ins[0].W, "chain inputs must share H, W");
+    P.seg[s] = {ins[s].p, ins[s].C, ins[s].bs};
+    cin += ins[s].C;
+  }
+  MLIC_CHECK(cin == c.cin0, "chain Cin mismatch");
+  MLIC_CHECK(out.C == c.cout[c.nl - 1] && out.H == ins[0].H && out.W == ins[0].W, "chain output shape");
+  P.cin0 = cin;
+  P.HW = ins[0].H * ins[0].W;
+  P.B = L().B;
+  for (int l = 0; l < 4; ++l) P.bias[l] = c.bias[l];
+  P.gelu_mask = (1 << (c.nl - 1)) - 1;
+  P.wimg = c.wimg;
+  P.out = out.p;
+  P.out_bs = out.bs;
+  if (res) {
+    MLIC_CHECK(res->C == out.C && res->H == out.H && res->W == out.W, "chain residual shape");
+    P.res = res->p;
+    P.res_bs = res->bs;
+  }
+  double mac = (double)c.cin0 * c.cout[0];
+  for (int l = 1; l < c.nl; ++l) mac += (double)c.cout[l - 1] * c.cout[l];
+  const double pix = (double)P.B * P.HW;
+  const double bytes = 4.0 * (pix * (cin + out.C * (res ? 2 : 1)) + mac);
+  timed(PCAT_CHAIN, 2.0 * mac * pix, bytes, [&] { chain_forward(P, c.nl, c.cout, L().st); }, c.name);
 }
 
 // conv3x3 of the fork (modules/layers/conv.py:22-32): DepthWiseConv (dw 3x3 -> pw 1x1) by default,
@@ -661,8 +756,13 @@ View Model::local_context(const View& x, int i) {
   timed(PCAT_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
     ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, L().B, L().st);
   }, p + ".norm2");
-  View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
-  conv({h1}, cw(p + ".mlp.fc2"), 1, 0, out, EPI_NONE, nullptr, &pj);
+  auto ch = chains_.find(p + ".mlp");
+  if (chain_on() && ch != chains_.end() && (H * W) % 4 == 0) {
+    run_chain(ch->second, {n2}, out, &pj);
+  } else {
+    View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
+    conv({h1}, cw(p + ".mlp.fc2"), 1, 0, out, EPI_NONE, nullptr, &pj);
+  }
   L().arena.release(m);
   return out;
 }
@@ -773,6 +873,11 @@ View Model::entropy_parameters(const std::vector<View>& ins, const std::string& 
   const int H = ins[0].H, W = ins[0].W;
   const ConvW& l3 = cw(p + ".6");
   View out = alloc(l3.Cout, H, W);
+  auto ch = chains_.find(p);
+  if (chain_on() && ch != chains_.end() && (H * W) % 4 == 0) {
+    run_chain(ch->second, ins, out, nullptr);
+    return out;
+  }
   const size_t m = L().arena.mark();
   View a = alloc(cw(p + ".0").Cout, H, W);
   conv(ins, cw(p + ".0"), 1, 0, a, EPI_GELU);

@@ -35,6 +35,15 @@ struct ConvW {
   std::string name;          // state_dict prefix (profiling)
 };
 
+// a fused 1x1 chain (chain.hip): EntropyParameters' 4 layers or LocalContext's MLP
+struct ChainW {
+  _Float16* wimg = nullptr;  // per-layer LDS images, concatenated
+  int nl = 0, cin0 = 0;
+  int cout[4] = {0, 0, 0, 0};
+  const float* bias[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::string name;
+};
+
 enum Precision : int { PREC_F32 = 0, PREC_F16X3 = 1, PREC_F16X3_V2 = 2 };
 struct DwW {
   const float* w = nullptr;  // [C][9]
@@ -158,6 +167,10 @@ class Model {
   enum class Mode { Forward, Encode, Decode };
   Cfg cfg_;
   std::map<std::string, ConvW> convs_;
+  std::map<std::string, ChainW> chains_;  // keyed by the module prefix (".fusion" / ".mlp")
+  void add_chains(hipStream_t st);
+  void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res);
+  bool chain_on() const;
   std::map<std::string, DwW> dws_;
   std::map<std::string, const float*> raw_;
   std::vector<void*> owned_;
