@@ -63,9 +63,10 @@ __device__ __forceinline__ void chain_wait(int n) {
   }
 }
 
-__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l) {
+__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l, int* rflag) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
+    range_check(rflag, v[e]);
     const _Float16 hv = (_Float16)v[e];
     h[e] = hv;
     l[e] = (_Float16)(v[e] - (float)hv);
@@ -82,10 +83,11 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   constexpr int B_OFF = F_OFF + 2 * CH_FSLOT;
   constexpr int NB = C1 + C2 + C3 + C4;
   static_assert(C1 % 32 == 0 && C2 % 16 == 0 && (C3 == 0 || C3 % 16 == 0) && (C4 == 0 || C4 % 16 == 0), "dims");
-  static_assert(B_OFF + NB * 4 <= 160 * 1024, "chain LDS");
+  static_assert(B_OFF + NB * 8 <= 160 * 1024, "chain LDS");
   static_assert(NL == 2 || C2 % 32 == 0, "inner layers feed whole K chunks");
-  __shared__ __attribute__((aligned(1024))) char sm[B_OFF + NB * 4];
+  __shared__ __attribute__((aligned(1024))) char sm[B_OFF + NB * 8];
   float* sbias = reinterpret_cast<float*>(sm + B_OFF);
+  float* sscale = sbias + NB;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = lane >> 4, l16 = lane & 15;
@@ -102,7 +104,10 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     int off = 0;
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-      for (int i = tid; i < CS[l]; i += CH_T) sbias[off + i] = P.bias[l] ? P.bias[l][i] : 0.0f;
+      for (int i = tid; i < CS[l]; i += CH_T) {
+        sbias[off + i] = P.bias[l] ? P.bias[l][i] : 0.0f;
+        sscale[off + i] = P.wscale[l] ? P.wscale[l][i] : 1.0f;
+      }
       off += CS[l];
     }
   }
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
         const int k = 8 * G + kk;
         v[kk] = *reinterpret_cast<const float*>(Fs + (k >> 1) * CH_FPAIR + (k & 1) * 512 + px * 4);
       }
-      split8(v, bh[j], bl[j]);
+      split8(v, bh[j], bl[j], P.rflag);
     }
 #pragma unroll
     for (int i = 0; i < C1 / 16; ++i) {
@@ -212,10 +217,11 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
         for (int q = 0; q < 2; ++q)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float x = acc[2 * c + q][j][e] + sbias[boff + 32 * c + 16 * q + 4 * G + e];
+            const int r = boff + 32 * c + 16 * q + 4 * G + e;
+            float x = acc[2 * c + q][j][e] * sscale[r] + sbias[r];
             v[4 * q + e] = gelu ? gelu_erf(x) : x;
           }
-        split8(v, oh[c][j], ol[c][j]);
+        split8(v, oh[c][j], ol[c][j], P.rflag);
       }
   };
 
@@ -252,7 +258,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = 16 * i + 4 * G + e;
-          float v = acc[i][j][e] + sbias[boff + co];
+          float v = acc[i][j][e] * sscale[boff + co] + sbias[boff + co];
           if (P.res) v += P.res[(int64_t)b * P.res_bs + (int64_t)co * HW + px];
           P.out[(int64_t)b * P.out_bs + (int64_t)co * HW + px] = v;
         }

@@ -69,7 +69,12 @@ int64_t conv_ws_bytes(int impl, const ConvParams& P, const ConvWeights& w) {
   return impl == CONV_X4 ? 2 * x4_act_halves(P, w.cin_pad) : 0;
 }
 
-void conv_run(int impl, const ConvParams& P, const ConvWeights& w, hipStream_t st, void* ws) {
+void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t st, void* ws) {
+  // the split-fp16 families read the prescaled hi/lo weights: their epilogues undo the row scale;
+  // the fp32 families read the unscaled fp32 weights
+  ConvParams P = P0;
+  const bool split = impl == CONV_X3 || impl == CONV_X3V2 || impl == CONV_PW || impl == CONV_HALO || impl == CONV_X4;
+  P.wscale = split ? w.ws : nullptr;
   switch (impl) {
     case CONV_F32: conv_forward(P, st); break;
     case CONV_X3: conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, st); break;

@@ -1,12 +1,18 @@
 // Implicit-GEMM convolution on the fp16 MFMA pipe with a 3-term split ("f16x3"), gfx950.
 //
-// Each fp32 operand is split exactly as  v = hi + lo + r  with hi = fp16(v), lo = fp16(v - hi),
-// |r| <= 2^-22 |v|, and  a.b  is computed as  lo_a.hi_b + hi_a.lo_b + hi_a.hi_b  by three
-// v_mfma_f32_32x32x16_f16 with fp32 accumulation (fp16 products are exact in fp32).  The dropped
-// terms are O(2^-22) relative, i.e. below fp32 summation-order noise (measured on the
-// oracle, delta-bpp 0, delta-PSNR 0, x_hat 4e-6), at 3/16 of the fp32-MFMA cost per FLOP:
-// 16384 MAC per 32-cycle f16 MFMA vs 2048 per 64-cycle f32 MFMA => 5.3x the fp32 peak.
-// Range: operands must stay inside fp16's range (|v| < 65504), true for this model's activations.
+// Each fp32 operand is split as  v = hi + lo + r  with hi = fp16(v), lo = fp16(v - hi), and  a.b  is
+// computed as  lo_a.hi_b + hi_a.lo_b + hi_a.hi_b  by three fp16 MFMAs with fp32 accumulation (fp16
+// products are exact in fp32), at 3/16 of the fp32-MFMA cost per FLOP.  Error of the split:
+//  * |r| <= 2^-22 |v| while lo is a normal fp16, i.e. |v| >= 2^-3 (lo ~ 2^-11 v >= 2^-14); below that
+//    lo is subnormal and |r| <= 2^-25 absolute.  Weights are therefore prescaled per output row by an
+//    exact power of two (split_weights, max|w_row| -> [2^14, 2^15)) and the scale is undone on the fp32
+//    accumulator, so every weight within 2^17 of its row's largest splits to 2^-22.  Activations are
+//    split unscaled: 2^-22 relative for |v| >= 2^-3, 2^-25 absolute below (below fp32's own 2^-24
+//    rounding of the dot product once the typical activation is >= 0.5).
+//  * |v| >= 65520 overflows fp16 (GDN squares its input: |x| >= 256): the split sites count such
+//    values in a device flag (range_flag) and the executor re-runs the call on the exact fp32 MFMA
+//    path (Model::guarded).
+// Measured on the oracle at 256x384 MLICPP_L: delta-bpp 0, delta-PSNR 0, x_hat 4e-6.
 //
 // GEMM view as conv_mfma.hip: out[co, p] = sum_k W[co, k] X[k, p], k = (tap, ci); tiles BM x BN x
 // BK(=32); LDS images are k-contiguous ([row][k], 80-byte pitch => conflict-free ds_read_b128 for
@@ -133,6 +139,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float v = rb[g + j];
+        range_check(P.rflag, v);
         const _Float16 hv = (_Float16)v;
         h[j] = hv;
         l[j] = (_Float16)(v - (float)hv);
@@ -203,6 +210,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
         const int co = co0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         if (co >= P.Cout) continue;
         float v = acc[i][j][r];
+        if (P.wscale) v *= P.wscale[co];
         if (P.bias) v += P.bias[co];
         if (epi & EPI_GELU) v = gelu_erf(v);
         if (epi & (EPI_GDN | EPI_IGDN)) {
@@ -403,6 +411,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
       half4 h, l;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        range_check(P.rflag, rb[r][q]);
         const _Float16 hv = (_Float16)rb[r][q];
         h[q] = hv;
         l[q] = (_Float16)(rb[r][q] - (float)hv);
@@ -479,6 +488,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
         const int co = co0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         if (co >= P.Cout) continue;
         float v = acc[i][j][r];
+        if (P.wscale) v *= P.wscale[co];
         if (P.bias) v += P.bias[co];
         if (epi & EPI_GELU) v = gelu_erf(v);
         if (epi & (EPI_GDN | EPI_IGDN)) {
@@ -533,6 +543,7 @@ static ConvParams cout_slice(const ConvParams& P, int r0, int n) {
   Q.Cout = n;
   Q.out = P.out + oc;
   if (P.bias) Q.bias = P.bias + r0;
+  if (P.wscale) Q.wscale = P.wscale + r0;
   if (P.aux) Q.aux = P.aux + (int64_t)r0 * HWo;
   if (P.res) Q.res = P.res + oc;
   return Q;
@@ -562,26 +573,59 @@ void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
   }
 }
 
-// weights [Cout][Cin][K][K] fp32 -> hi/lo fp16 [Cout][K*K][cin_pad] (zero padded)
+// Exact per-output-row power-of-two prescale of the split weights: row co is multiplied by 2^e with
+// max|w_co| * 2^e in [2^14, 2^15), so hi = fp16(v) and lo = fp16(v - hi) are both normal for every
+// weight within 2^17 of the row's largest (|r| <= 2^-22 |v| there; an unscaled 0.05 weight would
+// leave lo subnormal, ~2^-20), and nothing overflows.  wscale[co] = 2^-e is applied to the fp32
+// accumulator in the epilogue (exact).  Rows of zeros keep e = 0.
+__global__ void weight_row_scale_kernel(const float* __restrict__ w, int per_row, float* __restrict__ wscale) {
+  __shared__ float red[256];
+  const int co = blockIdx.x;
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < per_row; i += 256) m = fmaxf(m, fabsf(w[(int64_t)co * per_row + i]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + k]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int e = 0;
+    if (red[0] > 0.0f && isfinite(red[0])) {
+      int ex;
+      frexpf(red[0], &ex);  // max = f * 2^ex, f in [0.5, 1)  ->  max * 2^(15 - ex) in [2^14, 2^15)
+      e = min(max(15 - ex, -60), 60);
+    }
+    wscale[co] = ldexpf(1.0f, -e);
+  }
+}
+
+// weights [Cout][Cin][K][K] fp32 -> hi/lo fp16 [Cout][K*K][cin_pad] (zero padded), rows prescaled by
+// 1 / wscale[co] when wscale is given
 __global__ void split_weights_kernel(const float* __restrict__ w, _Float16* __restrict__ wh, _Float16* __restrict__ wl,
-                                     int Cout, int Cin, int KK, int cin_pad) {
+                                     int Cout, int Cin, int KK, int cin_pad, const float* __restrict__ wscale) {
   const int64_t n = (int64_t)Cout * KK * cin_pad;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int ci = (int)(i % cin_pad);
   const int tap = (int)((i / cin_pad) % KK);
   const int co = (int)(i / ((int64_t)cin_pad * KK));
-  const float v = ci < Cin ? w[((int64_t)co * Cin + ci) * KK + tap] : 0.0f;
+  float v = ci < Cin ? w[((int64_t)co * Cin + ci) * KK + tap] : 0.0f;
+  if (wscale) v = v / wscale[co];  // exact: a power of two
   const _Float16 h = (_Float16)v;
   wh[i] = h;
   wl[i] = (_Float16)(v - (float)h);
 }
 
-void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad,
+void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad, float* wscale,
                    hipStream_t st) {
+  if (wscale) {
+    hipLaunchKernelGGL(weight_row_scale_kernel, dim3(Cout), dim3(256), 0, st, w, Cin * KK, wscale);
+    HIP_OK(hipGetLastError());
+  }
   const int64_t n = (int64_t)Cout * KK * cin_pad;
   hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, wh, wl, Cout, Cin,
-                     KK, cin_pad);
+                     KK, cin_pad, (const float*)wscale);
   HIP_OK(hipGetLastError());
 }
 

@@ -145,6 +145,7 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
     half8 h, l;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+      range_check(P.rflag, v8[j]);
       const _Float16 hv = (_Float16)v8[j];
       h[j] = hv;
       l[j] = (_Float16)(v8[j] - (float)hv);

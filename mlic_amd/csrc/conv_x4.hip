@@ -270,6 +270,7 @@ struct X4Pack {
   Seg seg[MAXSEG];
   int nseg, Cin, H, W, pad, nchunk, square, npix;  // npix: real pixels (K = 1 folds H*W into rows of 32)
   _Float16* dst;
+  int* rflag;
 };
 
 // grid (ceil(Hp*Wp / 64), nchunk, B), 256 threads: lane = position (64 consecutive), wave = 8-channel group
@@ -293,6 +294,7 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
     const bool ok = inb && ch0 + j < Q.Cin && ch0 - c0 + j < sg.C;
     float v = ok ? src[(int64_t)j * HW] : 0.0f;
     if (Q.square) v *= v;
+    range_check(Q.rflag, v);
     const _Float16 hv = (_Float16)v;
     h[j] = hv;
     l[j] = (_Float16)(v - (float)hv);
@@ -379,6 +381,7 @@ void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st
   Q.nchunk = cin_pad / 32;
   Q.square = (P.epi & EPI_SQUARE_IN) ? 1 : 0;
   Q.dst = dst;
+  Q.rflag = P.rflag;
   const int npos = (Q.H + 2 * Q.pad) * (Q.W + 2 * Q.pad);
   hipLaunchKernelGGL(x4_pack_act_kernel, dim3((npos + 63) / 64, Q.nchunk, P.B), dim3(256), 0, st, Q);
   HIP_OK(hipGetLastError());

@@ -17,7 +17,8 @@ int conv_f16x3_variant(const ConvParams& P);
 void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 int conv_x3v2_variant(const ConvParams& P);
 void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
-void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad,
+// wscale (optional, [Cout]): receives 2^-e of the exact per-row prescale applied before the split
+void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad, float* wscale,
                    hipStream_t st);
 
 // specialised convs (conv_pw.hip)
@@ -52,6 +53,7 @@ struct ConvWeights {
   const _Float16* wl;
   int cin_pad;
   const _Float16* wx4 = nullptr;  // x4_pack_weights image (null: CONV_X4 not available)
+  const float* ws = nullptr;      // per-row prescale of wh/wl (split_weights), applied by the split paths
 };
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision);
 // device workspace conv_run needs for impl (bytes; 0 = none)
@@ -182,12 +184,14 @@ struct ChainParams {
   int nseg, cin0;  // layer-0 input: channel concat, cin0 % 32 == 0
   int HW, B;       // pixels per image (HW % 4 == 0)
   const float* bias[4];
+  const float* wscale[4];  // per-row prescale of each layer's split weights (split_weights), or null
   int gelu_mask;   // bit l: GELU after layer l (l < nl - 1)
   const _Float16* wimg;
   float* out;      // [B][cout[nl-1]][HW] (batch stride out_bs)
   int64_t out_bs;
   const float* res;  // optional residual added to the output (same layout, batch stride res_bs)
   int64_t res_bs;
+  int* rflag;        // fp16 range guard (common.h range_check)
 };
 bool chain_supported(int nl, const int* cout);
 int64_t chain_layer_halves(int Cout, int Cin);

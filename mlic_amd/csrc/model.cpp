@@ -68,11 +68,11 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     total += ((size_t)e * 4 + 255) & ~(size_t)255;
   }
   for (int i = 0; i < n; ++i) {
-    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(2 * numel[i] + shapes[i * 4]) * 4 + 1024;
+    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(2 * numel[i] + 2 * shapes[i * 4]) * 4 + 1280;
     if (ends_with(names[i], ".weight") && (ndims[i] == 4 || ndims[i] == 2)) {
       // split fp16 copy: 2 x Cout x KK x cin_pad halves
       const int64_t cout = shapes[i * 4], per = numel[i] / std::max<int64_t>(1, cout);
-      total += (size_t)(cout * (per + 32 * 25)) * 4 + 1024;
+      total += (size_t)(cout * (per + 32 * 25)) * 4 + 1024 + (size_t)cout * 4 + 256;
     }
   }
   total += 64 * 4 + 625 * 4 + 1024;
@@ -80,6 +80,9 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
   HIP_OK(hipMalloc(&block, total));
   owned_.push_back(block);
   wbytes_ = total;
+  HIP_OK(hipMalloc(&rflag_, sizeof(int)));
+  owned_.push_back(rflag_);
+  HIP_OK(hipMemsetAsync(rflag_, 0, sizeof(int), st));
   size_t off = 0;
   auto take = [&](int64_t nf) {
     char* p = block + off;
@@ -128,7 +131,8 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
         const int64_t nh = (int64_t)w.Cout * w.K * w.K * w.cin_pad;
         w.wh = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
         w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
-        split_weights(ptrs[i], w.wh, w.wl, w.Cout, w.Cin, w.K * w.K, w.cin_pad, st);
+        w.ws = take(w.Cout);
+        split_weights(ptrs[i], w.wh, w.wl, w.Cout, w.Cin, w.K * w.K, w.cin_pad, w.ws, st);
       }
       w.name = base;
       convs_[base] = w;
@@ -169,8 +173,9 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     const int64_t nh = (int64_t)C * w.cin_pad;
     w.wh = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
     w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
+    w.ws = take(C);
     MLIC_CHECK(off <= total, "weight block");
-    split_weights(gamma_eff, w.wh, w.wl, C, C, 1, w.cin_pad, st);
+    split_weights(gamma_eff, w.wh, w.wl, C, C, 1, w.cin_pad, w.ws, st);
     w.name = p + ".__gdn";
     convs_[p + ".__gdn"] = w;
   }
@@ -226,7 +231,7 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
       for (int cell = 0; cell < 25; ++cell) wp[(size_t)co * CIN + cell * 32 + c] = w[(size_t)co * CIN + c * 25 + cell];
   const int64_t nh = (int64_t)Cout * CIN, nx = x4_weight_halves(Cout, 1, CIN);
   char* blk = nullptr;
-  const size_t bytes = (size_t)nh * 4 + 2 * (size_t)nh * 2 + (size_t)nx * 2 + 1024;
+  const size_t bytes = (size_t)nh * 4 + 2 * (size_t)nh * 2 + (size_t)nx * 2 + (size_t)Cout * 4 + 2048;
   HIP_OK(hipMalloc(&blk, bytes));
   owned_.push_back(blk);
   wbytes_ += bytes;
@@ -234,8 +239,9 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
   _Float16* wh = reinterpret_cast<_Float16*>(blk + (size_t)nh * 4);
   _Float16* wl = wh + nh;
   _Float16* wx = reinterpret_cast<_Float16*>((reinterpret_cast<uintptr_t>(wl + nh) + 255) & ~(uintptr_t)255);
+  float* wsc = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(wx + nx) + 255) & ~(uintptr_t)255);
   HIP_OK(hipMemcpyAsync(wf, wp.data(), wp.size() * 4, hipMemcpyHostToDevice, st));
-  split_weights(wf, wh, wl, Cout, CIN, 1, CIN, st);
+  split_weights(wf, wh, wl, Cout, CIN, 1, CIN, wsc, st);
   x4_pack_weights(wh, wl, Cout, 1, CIN, wx, st);
   HIP_OK(hipStreamSynchronize(st));  // the host staging vectors die here
   ConvW cw;
@@ -247,6 +253,7 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
   cw.wl = wl;
   cw.cin_pad = CIN;
   cw.wx4 = wx;
+  cw.ws = wsc;
   cw.name = base;
   convs_[base + ".__x4perm"] = cw;
 }
@@ -278,6 +285,7 @@ void Model::add_chains(hipStream_t st) {
       const ConvW& w = it->second;
       c.cout[l] = w.Cout;
       c.bias[l] = w.b;
+      c.ws[l] = w.ws;
       if (l == 0) c.cin0 = w.Cin;
       else if (w.Cin != c.cout[l - 1]) ok = false;
       total += chain_layer_halves(w.Cout, w.Cin);
@@ -404,7 +412,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
                       const View& out2, int epi2) {
   const ConvParams P1 = conv_params(ins, w1, 1, w1.K / 2, out1, epi1, nullptr, nullptr);
   const ConvParams P2 = conv_params(ins, w2, 1, w2.K / 2, out2, epi2, nullptr, nullptr);
-  const ConvWeights c1{w1.w, w1.wh, w1.wl, w1.cin_pad, w1.wx4}, c2{w2.w, w2.wh, w2.wl, w2.cin_pad, w2.wx4};
+  const ConvWeights c1{w1.w, w1.wh, w1.wl, w1.cin_pad, w1.wx4, w1.ws}, c2{w2.w, w2.wh, w2.wl, w2.cin_pad, w2.wx4, w2.ws};
   if (conv_select(P1, c1, precision_) != CONV_X4 || conv_select(P2, c2, precision_) != CONV_X4 ||
       w1.cin_pad != w2.cin_pad || w1.K != w2.K) {
     run_conv(P1, w1, nullptr);
@@ -422,7 +430,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
 
 // packed: the input already in x4's split layout (conv_pair); the impl is then necessarily x4
 void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed) {
-  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4};
+  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4, w.ws};
   const int impl = packed ? CONV_X4 : conv_select(P, cw, precision_);
   const double outn = (double)P.B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * P.Cin * w.K * w.K;
@@ -461,6 +469,8 @@ ConvParams Model::conv_params(const std::vector<View>& ins, const ConvW& w, int 
   P.Ho = (P.H + 2 * pad - w.K) / stride + 1;
   P.Wo = (P.W + 2 * pad - w.K) / stride + 1;
   P.wpk = w.w;
+  P.wscale = w.ws;  // conv_run clears it for the fp32 families
+  P.rflag = rflag_;
   P.bias = w.b;
   P.epi = epi;
   if (epi & EPI_SHUFFLE) {
@@ -528,9 +538,13 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   P.cin0 = cin;
   P.HW = ins[0].H * ins[0].W;
   P.B = L().B;
-  for (int l = 0; l < 4; ++l) P.bias[l] = c.bias[l];
+  for (int l = 0; l < 4; ++l) {
+    P.bias[l] = c.bias[l];
+    P.wscale[l] = c.ws[l];
+  }
   P.gelu_mask = (1 << (c.nl - 1)) - 1;
   P.wimg = c.wimg;
+  P.rflag = rflag_;
   P.out = out.p;
   P.out_bs = out.bs;
   if (res) {
@@ -1230,7 +1244,7 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
   } restore{l, own};
   l.st = st;  // caller's stream, including the legacy NULL stream torch uses by default
   set_vbr(vbr_scales, B);
-  planned(B, st, [&] {
+  auto body = [&] {
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
     View z = h_a(y);
@@ -1243,7 +1257,38 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
       View out{x_hat, 3, H, W, (int64_t)3 * H * W};
       g_s(yhat, out);
     }
-  });
+  };
+  planned(B, st, body);
+  if (precision_ != PREC_F32 && range_hit(st)) {
+    // an activation left fp16's range in a split-fp16 kernel: the whole call again in exact fp32 MFMA
+    const int keep = precision_;
+    precision_ = PREC_F32;
+    try {
+      planned(B, st, body);
+    } catch (...) {
+      precision_ = keep;
+      throw;
+    }
+    precision_ = keep;
+    (void)range_hit(st);
+  }
+}
+
+// the fp16 range guard (common.h range_check): read and clear the device flag (synchronises `st`)
+bool Model::range_hit(hipStream_t st) {
+  int h = 0;
+  HIP_OK(hipMemcpyAsync(&h, rflag_, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (h) HIP_OK(hipMemsetAsync(rflag_, 0, sizeof(int), st));
+  return h != 0;
+}
+
+// compress/decompress cannot fall back silently: the decoder has to reproduce the encoder's exact
+// entropy parameters, so both sides must run the same arithmetic
+void Model::range_fail(hipStream_t st) {
+  if (precision_ != PREC_F32 && range_hit(st))
+    throw Error("mlic: an activation exceeded the fp16 range of the split-fp16 kernels (|v| >= 65504); "
+                "encode and decode this input with set_precision(0) (exact fp32 MFMA)");
 }
 
 void Model::compress(const float* x, int B, int H, int W, const float* vbr_scales, hipStream_t st) {
@@ -1256,6 +1301,7 @@ void Model::compress(const float* x, int B, int H, int W, const float* vbr_scale
     compress_lane(x + first * img, cnt, H, W);
     for (int b = 0; b < cnt; ++b) enc_all_[first + b] = std::move(l.enc[b]);
   });
+  range_fail(st);
 }
 
 // mlicpp.py:199-290 for the lane's images: network on the lane stream, then one host thread per
@@ -1351,6 +1397,7 @@ void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_
     set_vbr(vbr_scales ? vbr_scales + first : nullptr, cnt);
     decompress_lane(y + first, ylen + first, z + first, zlen + first, cnt, hz, wz, x_hat + first * img);
   });
+  range_fail(st);
 }
 
 // mlicpp.py:292-378 for the lane's images: z decoded on the host, then 20 phases of

@@ -32,6 +32,7 @@ struct ConvW {
   _Float16* wl = nullptr;
   int cin_pad = 0;
   _Float16* wx4 = nullptr;   // x4 LDS-image weights [ct][step][BM][64]     (conv_x4 path)
+  float* ws = nullptr;       // [Cout] 2^-e of the exact per-row prescale of wh/wl (split_weights)
   std::string name;          // state_dict prefix (profiling)
 };
 
@@ -41,6 +42,7 @@ struct ChainW {
   int nl = 0, cin0 = 0;
   int cout[4] = {0, 0, 0, 0};
   const float* bias[4] = {nullptr, nullptr, nullptr, nullptr};
+  const float* ws[4] = {nullptr, nullptr, nullptr, nullptr};
   std::string name;
 };
 
@@ -169,6 +171,9 @@ class Model {
   std::map<std::string, ConvW> convs_;
   std::map<std::string, ChainW> chains_;  // keyed by the module prefix (".fusion" / ".mlp")
   void add_chains(hipStream_t st);
+  int* rflag_ = nullptr;  // device fp16 range flag (common.h range_check)
+  bool range_hit(hipStream_t st);
+  void range_fail(hipStream_t st);
   void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res);
   bool chain_on() const;
   std::map<std::string, DwW> dws_;

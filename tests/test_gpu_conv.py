@@ -29,13 +29,14 @@ def reference(x, w, b, stride, epi, res):
     return y
 
 
-def run(impl, B, Cin, Cout, H, W, K, stride=1, epi=0, seed=0):
+def run(impl, B, Cin, Cout, H, W, K, stride=1, epi=0, seed=0, wmul=1.0, xmul=1.0):
     from mlic_amd import _lib
     g = torch.Generator().manual_seed(seed)
     dev = torch.device("cuda")
     x = (torch.rand(B, Cin, H, W, generator=g) - 0.5).to(dev)
     w = ((torch.rand(Cout, Cin, K, K, generator=g) - 0.5) / (Cin * K * K) ** 0.5).to(dev)
     b = (torch.rand(Cout, generator=g) - 0.5).to(dev)
+    x, w = x * xmul, w * wmul
     if epi & (GDN | IGDN):  # GDN: gamma >= 0, beta > 0 (compressai reparametrisation keeps them so)
         x = x * 4
         w = w.abs() * 0.1
@@ -282,3 +283,14 @@ def test_local_attention_packed(H, W, B):
     d = (got - expect).abs()
     assert d.mean().item() <= 1e-5 * expect.abs().mean().item() + 1e-7, d.mean().item()
     assert d.max().item() <= 1e-3 * expect.abs().max().item(), d.max().item()
+
+
+# split-fp16 operand range (conv_f16x3.hip header): tiny weights (the per-row power-of-two prescale keeps
+# their lo halves normal) and activations up to 1e3, every split family, against float64
+@pytest.mark.parametrize("impl,Cin,Cout,H,W,K", [(X3V2, 192, 320, 24, 40, 1), (X3V2, 96, 96, 20, 36, 3),
+                                                 (PW, 192, 192, 36, 60, 1), (X4, 192, 768, 16, 64, 3),
+                                                 (HALO, 96, 96, 24, 64, 5)])
+@pytest.mark.parametrize("wmul,xmul", [(1e-3, 2e3), (1e-4, 1.0), (3e-5, 5e2)])
+def test_split_operand_range(impl, Cin, Cout, H, W, K, wmul, xmul):
+    y, ref = run(impl, 2, Cin, Cout, H, W, K, wmul=wmul, xmul=xmul)
+    check(y, ref, rtol=2e-5)

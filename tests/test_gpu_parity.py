@@ -466,3 +466,58 @@ def test_4k_parity_and_roundtrip():
     c = net.compress(x.to(DEV))
     d = net.decompress(c["strings"], c["shape"])
     assert torch.equal(d["x_hat"], out["x_hat"])
+
+
+@pytest.mark.parametrize("kind,idx,cin", [("anchor", 0, 640), ("anchor", 5, 832), ("nonanchor", 0, 704),
+                                          ("nonanchor", 9, 960)])
+def test_entropy_parameters_chain_vs_oracle(kind, idx, cin):
+    """The fused EntropyParameters chain (4 layers, one kernel) against the oracle's layer-by-layer fp32
+    (entropy.py:7-29) on a batch of 2 with a ragged pixel tile (20 x 28 = 560 = 4 x 128 + 48)."""
+    net = net_for("MLICPP_L")
+    g = torch.Generator().manual_seed(31 + idx)
+    x = torch.randn(2, cin, 20, 28, generator=g) * 2
+    m = ref.RefMLIC("MLICPP_L", synthetic.synth_state_dict("MLICPP_L", 0))
+    with torch.no_grad():
+        exp = m.entropy_parameters(x, kind, idx)
+    got = net.run_module("epa" if kind == "anchor" else "epn", idx, x.to(DEV), out_shape=tuple(exp.shape)).cpu()
+    err = float((got - exp).abs().max())
+    PARITY[f"chain_ep_{kind}{idx}"] = {"max_abs_err": err, "max_abs": float(exp.abs().max())}
+    assert err <= 2e-5 * max(1.0, float(exp.abs().max())), PARITY[f"chain_ep_{kind}{idx}"]
+
+
+def test_local_context_chain_ragged_vs_oracle():
+    """LocalContext with its fused MLP chain at a ragged latent size, against the oracle."""
+    net = net_for("MLICPP_L")
+    g = torch.Generator().manual_seed(77)
+    x = ref.ckbd_anchor(torch.randn(2, 32, 12, 20, generator=g) * 3)
+    m = ref.RefMLIC("MLICPP_L", synthetic.synth_state_dict("MLICPP_L", 0))
+    with torch.no_grad():
+        exp = m.local_context(x, 4)
+    got = net.run_module("local", 4, x.to(DEV), out_shape=tuple(exp.shape)).cpu()
+    err = float((got - exp).abs().max())
+    PARITY["chain_local4"] = {"max_abs_err": err}
+    assert err <= 1e-4 * max(1.0, float(exp.abs().max()))
+
+
+def test_fp16_range_guard():
+    """An activation beyond fp16 (here GDN's squared input, |x| >> 256) in a split-fp16 kernel:
+    forward() re-runs on the exact fp32 MFMA path (result == the precision-0 forward, bit for bit);
+    compress() refuses loudly (the decoder must reproduce the encoder's arithmetic)."""
+    from mlic_amd import _lib
+    name, H, W = "MLICPP_S", 128, 128
+    sd = synthetic.synth_state_dict(name, rate=1)
+    sd["g_a.analysis_transform.0.conv2.point_conv.weight"] = sd["g_a.analysis_transform.0.conv2.point_conv.weight"] * 5000
+    net = get_model(name)
+    net.load_state_dict(sd)
+    net = net.to(DEV).eval()
+    x = synthetic.synth_image(H, W, 4).to(DEV)
+    f = net(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(f["x_hat"]).all()
+    net.set_precision(0)
+    f0 = net(x)
+    assert torch.equal(f["x_hat"], f0["x_hat"])
+    net.set_precision(2)
+    net.update()
+    with pytest.raises(_lib.MlicError, match="fp16 range"):
+        net.compress(x)
