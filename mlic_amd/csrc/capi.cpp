@@ -252,9 +252,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
       HIP_OK(hipMemset(bias, 0, Cout * 4));
     }
     pack_conv(w, wp, Cout, Cin, K * K, nullptr);
-    float* wsc = nullptr;
-    HIP_OK(hipMalloc(&wsc, Cout * 4));
-    split_weights(w, wh, wl, Cout, Cin, K * K, cin_pad, wsc, nullptr);
+    const int wexp = split_weights(w, wh, wl, Cout, Cin, K * K, cin_pad, true, nullptr);
     ConvParams P{};
     P.nseg = 1;
     P.seg[0] = {x, Cin, (int64_t)Cin * H * W};
@@ -268,7 +266,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
       HIP_OK(hipMalloc((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2));
       x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, nullptr);
     }
-    const ConvWeights cw{wp, wh, wl, cin_pad, wx, wsc};
+    const ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
     const int which = impl == 3 ? conv_select(P, cw, 2) : impl;  // 3 = what the model runs (precision 2)
     if (which == CONV_X4) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
     void* ws = nullptr;
@@ -290,7 +288,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     *tflops = 2.0 * (double)B * Cout * Ho * Wo * Cin * K * K / (*ms_per * 1e-3) / 1e12;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl, (void*)wx, ws, (void*)wsc})
+    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl, (void*)wx, ws})
       if (p) (void)hipFree(p);
   });
 }
@@ -336,9 +334,7 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     HIP_OK(hipMallocAsync((void**)&wh, nh * 2, st));
     HIP_OK(hipMallocAsync((void**)&wl, nh * 2, st));
     pack_conv(w, wp, Cout, Cin, K * K, st);
-    float* wsc = nullptr;
-    HIP_OK(hipMallocAsync((void**)&wsc, Cout * 4, st));
-    split_weights(w, wh, wl, Cout, Cin, K * K, cin_pad, wsc, st);
+    const int wexp = split_weights(w, wh, wl, Cout, Cin, K * K, cin_pad, true, st);
     ConvParams P{};
     P.nseg = 1;
     P.seg[0] = {x, Cin, (int64_t)Cin * H * W};
@@ -357,7 +353,7 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
       HIP_OK(hipMallocAsync((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2, st));
       x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, st);
     }
-    const ConvWeights cw{wp, wh, wl, cin_pad, wx, wsc};
+    const ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
     const int which = impl < 0 ? conv_select(P, cw, 2) : impl;
     if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
     if (which == CONV_NARROW) MLIC_CHECK(conv_narrow_ok(P), "narrow: unsupported shape");
@@ -370,7 +366,6 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     conv_run(which, P, cw, st, ws);
     if (ws) HIP_OK(hipFreeAsync(ws, st));
     if (wx) HIP_OK(hipFreeAsync(wx, st));
-    HIP_OK(hipFreeAsync(wsc, st));
     HIP_OK(hipFreeAsync(wp, st));
     HIP_OK(hipFreeAsync(wh, st));
     HIP_OK(hipFreeAsync(wl, st));

@@ -17,11 +17,11 @@
 //     pre-packed on the host side into the exact LDS image (128-byte rows: hi of 32 k | lo of 32 k,
 //     16-byte granule G of row n at G ^ ((n >> 1) & 7): conflict-free ds_read_b128 fragments), moved
 //     by global_load_lds_dwordx4 (LDS-DMA) into a 3-slot ring, two steps ahead;
-//   * layer 0's input (fp32 NCHW, a multi-segment channel concat) streams by LDS-DMA as well, 32
-//     channels x 128 pixels per step into a 2-slot ring; each wave reads its B fragments from there and
-//     splits them in registers;
-//   * the K-step sequence of all layers is one pipeline: one counted `s_waitcnt vmcnt` and one raw
-//     s_barrier per step (no compiler-visible global load in the loop, so no hidden vmcnt(0)).
+//   * layer 0's input (fp32 NCHW, a multi-segment channel concat) is loaded by each lane straight into
+//     its B-fragment registers, three K-steps ahead (HBM latency), and split in registers;
+//   * the K-step sequence of all layers is one pipeline: one counted `s_waitcnt vmcnt` (weights of
+//     this step landed; the younger input loads and weight DMAs stay in flight) and one raw s_barrier
+//     per step.
 #include "common.h"
 #include "kernels.h"
 
@@ -36,8 +36,6 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 constexpr int CH_T = 256;      // threads (4 waves)
 constexpr int CH_BN = 128;     // pixels per workgroup
-constexpr int CH_FPAIR = 1040; // bytes per channel pair of the fp32 input slot (1 KB + 16: conflict-free b32 reads)
-constexpr int CH_FSLOT = 16 * CH_FPAIR;
 
 __device__ __forceinline__ int chswz(int row) { return (row >> 1) & 7; }
 
@@ -63,10 +61,10 @@ __device__ __forceinline__ void chain_wait(int n) {
   }
 }
 
-__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l, int* rflag) {
+__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l, bool& bad) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    range_check(rflag, v[e]);
+    bad |= f16_unsafe(v[e]);
     const _Float16 hv = (_Float16)v[e];
     h[e] = hv;
     l[e] = (_Float16)(v[e] - (float)hv);
@@ -79,15 +77,13 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   constexpr int NL = C4 ? 4 : (C3 ? 3 : 2);
   constexpr int CMAX = C1;  // layer 0 is the widest (checked by the host side)
   constexpr int WSLOT = CMAX * 128;
-  constexpr int F_OFF = 3 * WSLOT;
-  constexpr int B_OFF = F_OFF + 2 * CH_FSLOT;
+  constexpr int B_OFF = 3 * WSLOT;
   constexpr int NB = C1 + C2 + C3 + C4;
   static_assert(C1 % 32 == 0 && C2 % 16 == 0 && (C3 == 0 || C3 % 16 == 0) && (C4 == 0 || C4 % 16 == 0), "dims");
-  static_assert(B_OFF + NB * 8 <= 160 * 1024, "chain LDS");
+  static_assert(B_OFF + NB * 4 <= 160 * 1024, "chain LDS");
   static_assert(NL == 2 || C2 % 32 == 0, "inner layers feed whole K chunks");
-  __shared__ __attribute__((aligned(1024))) char sm[B_OFF + NB * 8];
+  __shared__ __attribute__((aligned(1024))) char sm[B_OFF + NB * 4];
   float* sbias = reinterpret_cast<float*>(sm + B_OFF);
-  float* sscale = sbias + NB;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = lane >> 4, l16 = lane & 15;
@@ -104,10 +100,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     int off = 0;
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-      for (int i = tid; i < CS[l]; i += CH_T) {
-        sbias[off + i] = P.bias[l] ? P.bias[l][i] : 0.0f;
-        sscale[off + i] = P.wscale[l] ? P.wscale[l][i] : 1.0f;
-      }
+      for (int i = tid; i < CS[l]; i += CH_T) sbias[off + i] = P.bias[l] ? P.bias[l][i] : 0.0f;
       off += CS[l];
     }
   }
@@ -139,26 +132,32 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     w_off += (int64_t)R * 64;
     ++w_next;
   };
-  // layer-0 input DMA: channels [32t, 32t + 32) x pixels [p0, p0 + 128) fp32 -> F slot t & 1,
-  // channel pair cp = 4 wv + i at cp * CH_FPAIR; lane: channel 2cp + (lane >> 5), pixels 4 (lane & 31) ..
-  auto issue_f = [&](int t) {
-    char* dst = sm + F_OFF + (t & 1) * CH_FSLOT;
-    const int px = min(p0 + 4 * (lane & 31), HW - 4);  // ragged last tile: clamped, outputs dropped
+  // layer-0 input: prefetched into registers 3 K-steps ahead (a 3-deep register ring, the loop below
+  // is unrolled by 3 so the ring index is static).  Lane (G, l16) loads exactly its B fragments:
+  // channels 32t + 8G .. +7 at pixels p0 + 32 wv + 16 j + l16 (16 dword loads; the 32 channels of a
+  // K-step lie in one input segment, segments being multiples of 32).  These loads are compiler-
+  // visible: the compiler's own vmcnt for them only over-waits (it does not see the DMAs), and the
+  // explicit per-step wait below counts them (NF per step).
+  constexpr int NF = 16;
+  auto load_f = [&](int t, float (&f)[2][8]) {
+    if (t >= S0) return;
+    const int ch = 32 * t;
+    int s = 0, c0 = 0;
+    while (s + 1 < P.nseg && ch >= c0 + P.seg[s].C) { c0 += P.seg[s].C; ++s; }
+    const float* src = P.seg[s].p + (int64_t)b * P.seg[s].bs + (int64_t)(ch - c0 + 8 * G) * HW;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cp = wv * 4 + i;
-      const int ch = 32 * t + 2 * cp + (lane >> 5);
-      int s = 0, c0 = 0;
-      while (s + 1 < P.nseg && ch >= c0 + P.seg[s].C) { c0 += P.seg[s].C; ++s; }
-      const float* src = P.seg[s].p + (int64_t)b * P.seg[s].bs + (int64_t)(ch - c0) * HW + px;
-      chain_glds(src, dst + cp * CH_FPAIR);
+    for (int j = 0; j < 2; ++j) {
+      const int px = min(p0 + 32 * wv + 16 * j + l16, HW - 1);  // ragged last tile: outputs dropped
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HW + px];
     }
   };
+  auto nf_of = [&](int t) { return t < S0 ? NF : 0; };
+  // at the top of step u only W(u) must have landed; issued after it: F(u+1), W(u+1), F(u+2)
   auto step_begin = [&](int t) {
-    chain_wait(rows_of(t + 1) / 32);  // F(t) and W(t) have landed (only W(t+1) may be younger)
+    chain_wait(nf_of(t + 1) + rows_of(t + 1) / 32 + nf_of(t + 2));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < S0) issue_f(t + 1);
     if (t + 2 < T) issue_w();
   };
 
@@ -167,46 +166,58 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
   };
+  // one K-step of COUT rows against B operands in registers; the A fragments of row block i + 1 are
+  // read while block i's MFMAs issue
+  auto kstep = [&](auto& acc, const char* As, const half8 (&bh)[2], const half8 (&bl)[2], auto cout_c) {
+    constexpr int COUT = decltype(cout_c)::value;
+    half8 ah[2], al[2];
+    ah[0] = chain_frag(As, l16, G);
+    al[0] = chain_frag(As, l16, G + 4);
+#pragma unroll
+    for (int i = 0; i < COUT / 16; ++i) {
+      if (i + 1 < COUT / 16) {
+        ah[(i + 1) & 1] = chain_frag(As, 16 * (i + 1) + l16, G);
+        al[(i + 1) & 1] = chain_frag(As, 16 * (i + 1) + l16, G + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) mfma3(acc[i][j], ah[i & 1], al[i & 1], bh[j], bl[j]);
+    }
+  };
 
-  // prologue: W(0), F(0), W(1)
+  bool bad = false;  // fp16 range guard (common.h)
+  // prologue, issued in the per-step order (step u issues W(u+2), then F(u+3)): F(0) W(0) F(1) W(1) F(2)
+  float fr[3][2][8];
+  load_f(0, fr[0]);
   issue_w();
-  issue_f(0);
+  load_f(1, fr[1]);
   if (T > 1) issue_w();
+  load_f(2, fr[2]);
 
-  // ------------------------------------------------------------------ layer 0 (input from LDS)
+  // ------------------------------------------------------------------ layer 0 (input prefetched)
   floatx4 acc0[C1 / 16][2];
 #pragma unroll
   for (int i = 0; i < C1 / 16; ++i)
     for (int j = 0; j < 2; ++j) acc0[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < S0; ++t) {
+  auto step0 = [&](int t, float (&f)[2][8]) {
+    if (t >= S0) return;
     step_begin(t);
-    const char* As = sm + (t % 3) * WSLOT;
-    const char* Fs = sm + F_OFF + (t & 1) * CH_FSLOT;
     half8 bh[2], bl[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float v[8];
-      const int px = 32 * wv + 16 * j + l16;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int k = 8 * G + kk;
-        v[kk] = *reinterpret_cast<const float*>(Fs + (k >> 1) * CH_FPAIR + (k & 1) * 512 + px * 4);
-      }
-      split8(v, bh[j], bl[j], P.rflag);
-    }
-#pragma unroll
-    for (int i = 0; i < C1 / 16; ++i) {
-      const half8 ah = chain_frag(As, 16 * i + l16, G), al = chain_frag(As, 16 * i + l16, G + 4);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) mfma3(acc0[i][j], ah, al, bh[j], bl[j]);
-    }
+    for (int j = 0; j < 2; ++j) split8(f[j], bh[j], bl[j], bad);
+    load_f(t + 3, f);  // the ring slot is free once split
+    kstep(acc0, sm + (t % 3) * WSLOT, bh, bl, std::integral_constant<int, C1>{});
+  };
+  for (int t = 0; t < S0; t += 3) {
+    step0(t, fr[0]);
+    step0(t + 1, fr[1]);
+    step0(t + 2, fr[2]);
   }
 
   using I1 = std::integral_constant<int, S1>;
   using I2 = std::integral_constant<int, S2>;
   using I3 = std::integral_constant<int, S3>;
   // accumulators of a layer -> the next layer's B operands (bias + GELU + split, in registers)
-  auto to_operands = [&](auto& acc, half8 (*oh)[2], half8 (*ol)[2], auto nch_c, int boff, bool gelu) {
+  auto to_operands = [&](auto& acc, half8 (*oh)[2], half8 (*ol)[2], auto nch_c, int boff, bool gelu, int wexp) {
     constexpr int NCH = decltype(nch_c)::value;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
@@ -218,10 +229,10 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = boff + 32 * c + 16 * q + 4 * G + e;
-            float x = acc[2 * c + q][j][e] * sscale[r] + sbias[r];
+            float x = ldexpf(acc[2 * c + q][j][e], -wexp) + sbias[r];
             v[4 * q + e] = gelu ? gelu_erf(x) : x;
           }
-        split8(v, oh[c][j], ol[c][j], P.rflag);
+        split8(v, oh[c][j], ol[c][j], bad);
       }
   };
 
@@ -235,20 +246,15 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     for (int c = 0; c < NCH; ++c) {
       const int t = t0 + c;
       step_begin(t);
-      const char* As = sm + (t % 3) * WSLOT;
-#pragma unroll
-      for (int i = 0; i < COUT / 16; ++i) {
-        const half8 ah = chain_frag(As, 16 * i + l16, G), al = chain_frag(As, 16 * i + l16, G + 4);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) mfma3(acc[i][j], ah, al, bh[c][j], bl[c][j]);
-      }
+      const half8 b_h[2] = {bh[c][0], bh[c][1]}, b_l[2] = {bl[c][0], bl[c][1]};
+      kstep(acc, sm + (t % 3) * WSLOT, b_h, b_l, cout_c);
     }
   };
-
   // the output of the last layer: bias (+ residual), fp32 NCHW store
-  auto store = [&](auto& acc, auto cout_c, int boff) {
+  auto store = [&](auto& acc, auto cout_c, int boff, int wexp) {
     constexpr int COUT = decltype(cout_c)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    range_report(P.rflag, bad);
 #pragma unroll
     for (int i = 0; i < COUT / 16; ++i)
 #pragma unroll
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = 16 * i + 4 * G + e;
-          float v = acc[i][j][e] * sscale[boff + co] + sbias[boff + co];
+          float v = ldexpf(acc[i][j][e], -wexp) + sbias[boff + co];
           if (P.res) v += P.res[(int64_t)b * P.res_bs + (int64_t)co * HW + px];
           P.out[(int64_t)b * P.out_bs + (int64_t)co * HW + px] = v;
         }
@@ -266,24 +272,24 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   };
 
   half8 b1h[C1 / 32][2], b1l[C1 / 32][2];
-  to_operands(acc0, b1h, b1l, I1{}, 0, (P.gelu_mask & 1) != 0);
+  to_operands(acc0, b1h, b1l, I1{}, 0, (P.gelu_mask & 1) != 0, P.wexp[0]);
   floatx4 acc1[C2 / 16][2];
   layer_regs(acc1, b1h, b1l, I1{}, std::integral_constant<int, C2>{}, S0);
   if constexpr (NL == 2) {
-    store(acc1, std::integral_constant<int, C2>{}, C1);
+    store(acc1, std::integral_constant<int, C2>{}, C1, P.wexp[1]);
   } else {
     half8 b2h[C2 / 32 > 0 ? C2 / 32 : 1][2], b2l[C2 / 32 > 0 ? C2 / 32 : 1][2];
-    to_operands(acc1, b2h, b2l, I2{}, C1, (P.gelu_mask & 2) != 0);
+    to_operands(acc1, b2h, b2l, I2{}, C1, (P.gelu_mask & 2) != 0, P.wexp[1]);
     floatx4 acc2[C3 / 16][2];
     layer_regs(acc2, b2h, b2l, I2{}, std::integral_constant<int, C3>{}, S0 + S1);
     if constexpr (NL == 3) {
-      store(acc2, std::integral_constant<int, C3>{}, C1 + C2);
+      store(acc2, std::integral_constant<int, C3>{}, C1 + C2, P.wexp[2]);
     } else {
       half8 b3h[C3 / 32][2], b3l[C3 / 32][2];
-      to_operands(acc2, b3h, b3l, I3{}, C1 + C2, (P.gelu_mask & 4) != 0);
+      to_operands(acc2, b3h, b3l, I3{}, C1 + C2, (P.gelu_mask & 4) != 0, P.wexp[2]);
       floatx4 acc3[C4 / 16][2];
       layer_regs(acc3, b3h, b3l, I3{}, std::integral_constant<int, C4>{}, S0 + S1 + S2);
-      store(acc3, std::integral_constant<int, C4>{}, C1 + C2 + C3);
+      store(acc3, std::integral_constant<int, C4>{}, C1 + C2 + C3, P.wexp[3]);
     }
   }
 }

@@ -75,7 +75,7 @@ struct ConvParams {
   int Cout, Ho, Wo;       // conv output grid (before pixel shuffle)
   int K, stride, pad;     // square kernel
   const float* wpk;       // packed weights [K*K][Cin][Cout]
-  const float* wscale;    // [Cout] 2^-e of the split weights' exact per-row prescale (split-fp16 paths), or null
+  int wexp;               // split-fp16 paths: the hi/lo weights are the layer's weights * 2^wexp (exact)
   const float* bias;      // [Cout] or null
   float* out;
   int64_t out_bs;         // batch stride of out (floats)
@@ -91,10 +91,12 @@ struct ConvParams {
 
 // device helpers -----------------------------------------------------------------------------
 // fp16 range guard at every activation split site: a value that does not fit fp16 (|v| >= 65520
-// rounds to inf; checked with margin, NaN included) raises *flag; the executor then re-runs forward
-// on the exact fp32 MFMA path, or fails compress/decompress loudly (Model::range_check)
-__device__ __forceinline__ void range_check(int* flag, float v) {
-  if (!(fabsf(v) < 65504.0f) && flag) atomicOr(flag, 1);
+// rounds to inf; NaN included) is noted in a per-thread bit, and range_report raises *flag once per
+// thread at the end of the kernel; the executor then re-runs forward on the exact fp32 MFMA path, or
+// fails compress/decompress loudly (Model::range_hit / range_fail)
+__device__ __forceinline__ bool f16_unsafe(float v) { return (__float_as_uint(v) & 0x7fffffffu) >= 0x477ff000u; }
+__device__ __forceinline__ void range_report(int* flag, bool bad) {
+  if (bad && flag) atomicOr(flag, 1);
 }
 __device__ __forceinline__ float gelu_erf(float x) {
   // torch.nn.GELU(): 0.5 * x * (1 + erf(x / sqrt(2)))
@@ -113,7 +115,7 @@ __device__ __forceinline__ bool is_anchor(int h, int w) { return ((h + w) & 1) =
 __device__ __forceinline__ void conv_store(const ConvParams& P, int b, int co, int p, float v) {
   const int epi = P.epi;
   const int HWo = P.Ho * P.Wo;
-  if (P.wscale) v *= P.wscale[co];
+  v = ldexpf(v, -P.wexp);
   if (P.bias) v += P.bias[co];
   if (epi & EPI_GELU) v = gelu_erf(v);
   if (epi & (EPI_GDN | EPI_IGDN)) {
@@ -155,10 +157,9 @@ __device__ __forceinline__ void conv_store4(const ConvParams& P, int b, int co, 
   const int epi = P.epi;
   float a[4] = {v.x, v.y, v.z, v.w};
   const float bi = P.bias ? P.bias[co] : 0.0f;
-  const float sc = P.wscale ? P.wscale[co] : 1.0f;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    a[e] = a[e] * sc + bi;
+    a[e] = ldexpf(a[e], -P.wexp) + bi;
     if (epi & EPI_GELU) a[e] = gelu_erf(a[e]);
   }
   if (epi & (EPI_GDN | EPI_IGDN)) {
@@ -193,8 +194,8 @@ __device__ __forceinline__ void conv_store_shuf4(const ConvParams& P, int b, int
   const int epi = P.epi;
   float a[4] = {v.x, v.y, v.z, v.w};
   const float b0 = P.bias ? P.bias[co0] : 0.0f, b1 = P.bias ? P.bias[co0 + 1] : 0.0f;
-  const float s0 = P.wscale ? P.wscale[co0] : 1.0f, s1 = P.wscale ? P.wscale[co0 + 1] : 1.0f;
-  a[0] = a[0] * s0 + b0; a[1] = a[1] * s1 + b1; a[2] = a[2] * s0 + b0; a[3] = a[3] * s1 + b1;
+  a[0] = ldexpf(a[0], -P.wexp) + b0; a[1] = ldexpf(a[1], -P.wexp) + b1;
+  a[2] = ldexpf(a[2], -P.wexp) + b0; a[3] = ldexpf(a[3], -P.wexp) + b1;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (epi & EPI_GELU) a[e] = gelu_erf(a[e]);

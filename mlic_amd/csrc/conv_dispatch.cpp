@@ -74,7 +74,7 @@ void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t 
   // the fp32 families read the unscaled fp32 weights
   ConvParams P = P0;
   const bool split = impl == CONV_X3 || impl == CONV_X3V2 || impl == CONV_PW || impl == CONV_HALO || impl == CONV_X4;
-  P.wscale = split ? w.ws : nullptr;
+  P.wexp = split ? w.wexp : 0;
   switch (impl) {
     case CONV_F32: conv_forward(P, st); break;
     case CONV_X3: conv_f16x3_forward(P, w.wh, w.wl, w.cin_pad, st); break;

@@ -4,9 +4,9 @@
 // computed as  lo_a.hi_b + hi_a.lo_b + hi_a.hi_b  by three fp16 MFMAs with fp32 accumulation (fp16
 // products are exact in fp32), at 3/16 of the fp32-MFMA cost per FLOP.  Error of the split:
 //  * |r| <= 2^-22 |v| while lo is a normal fp16, i.e. |v| >= 2^-3 (lo ~ 2^-11 v >= 2^-14); below that
-//    lo is subnormal and |r| <= 2^-25 absolute.  Weights are therefore prescaled per output row by an
-//    exact power of two (split_weights, max|w_row| -> [2^14, 2^15)) and the scale is undone on the fp32
-//    accumulator, so every weight within 2^17 of its row's largest splits to 2^-22.  Activations are
+//    lo is subnormal and |r| <= 2^-25 absolute.  Weights are therefore prescaled per layer by an exact
+//    power of two (split_weights, max|w| -> [2^14, 2^15)) and the scale is undone on the fp32
+//    accumulator, so every weight within 2^17 of its layer's largest splits to 2^-22.  Activations are
 //    split unscaled: 2^-22 relative for |v| >= 2^-3, 2^-25 absolute below (below fp32's own 2^-24
 //    rounding of the dot product once the typical activation is >= 0.5).
 //  * |v| >= 65520 overflows fp16 (GDN squares its input: |x| >= 256): the split sites count such
@@ -21,7 +21,10 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
+#include <algorithm>
 
 namespace mlic {
 
@@ -80,6 +83,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
 
   uint4 ra_h[A_CHUNKS], ra_l[A_CHUNKS];
   float rb[B_ROWS];
+  bool bad = false;
 
   auto load_tile = [&](int t) {
     const int tap = t / nck;
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float v = rb[g + j];
-        range_check(P.rflag, v);
+        bad |= f16_unsafe(v);
         const _Float16 hv = (_Float16)v;
         h[j] = hv;
         l[j] = (_Float16)(v - (float)hv);
@@ -195,6 +199,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
     __syncthreads();
   }
 
+  range_report(P.rflag, bad);
   // epilogue (C/D map of the 32x32 MFMAs: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5))
   const int epi = P.epi;
   const int khalf = lane >> 5;
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(XB_THREADS) void conv_f16x3_kernel(ConvParams P, co
         const int co = co0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         if (co >= P.Cout) continue;
         float v = acc[i][j][r];
-        if (P.wscale) v *= P.wscale[co];
+        v = ldexpf(v, -P.wexp);
         if (P.bias) v += P.bias[co];
         if (epi & EPI_GELU) v = gelu_erf(v);
         if (epi & (EPI_GDN | EPI_IGDN)) {
@@ -339,6 +344,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
 
   uint4 ra_h[A_CHUNKS], ra_l[A_CHUNKS];
   float rb[RPT][4];
+  bool bad = false;
 
   auto load_tile = [&](int t) {
     const int tap = t / nck;
@@ -411,7 +417,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
       half4 h, l;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        range_check(P.rflag, rb[r][q]);
+        bad |= f16_unsafe(rb[r][q]);
         const _Float16 hv = (_Float16)rb[r][q];
         h[q] = hv;
         l[q] = (_Float16)(rb[r][q] - (float)hv);
@@ -473,6 +479,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
     if (t + 1 < ntile) store_tile(cur ^ 1);
     __syncthreads();
   }
+  range_report(P.rflag, bad);
 
   const int epi = P.epi;
   const int khalf = lane >> 5;
@@ -488,7 +495,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
         const int co = co0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         if (co >= P.Cout) continue;
         float v = acc[i][j][r];
-        if (P.wscale) v *= P.wscale[co];
+        v = ldexpf(v, -P.wexp);
         if (P.bias) v += P.bias[co];
         if (epi & EPI_GELU) v = gelu_erf(v);
         if (epi & (EPI_GDN | EPI_IGDN)) {
@@ -543,7 +550,6 @@ static ConvParams cout_slice(const ConvParams& P, int r0, int n) {
   Q.Cout = n;
   Q.out = P.out + oc;
   if (P.bias) Q.bias = P.bias + r0;
-  if (P.wscale) Q.wscale = P.wscale + r0;
   if (P.aux) Q.aux = P.aux + (int64_t)r0 * HWo;
   if (P.res) Q.res = P.res + oc;
   return Q;
@@ -573,60 +579,65 @@ void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
   }
 }
 
-// Exact per-output-row power-of-two prescale of the split weights: row co is multiplied by 2^e with
-// max|w_co| * 2^e in [2^14, 2^15), so hi = fp16(v) and lo = fp16(v - hi) are both normal for every
-// weight within 2^17 of the row's largest (|r| <= 2^-22 |v| there; an unscaled 0.05 weight would
-// leave lo subnormal, ~2^-20), and nothing overflows.  wscale[co] = 2^-e is applied to the fp32
-// accumulator in the epilogue (exact).  Rows of zeros keep e = 0.
-__global__ void weight_row_scale_kernel(const float* __restrict__ w, int per_row, float* __restrict__ wscale) {
+// Exact power-of-two prescale of a layer's split weights: the layer is multiplied by 2^e with
+// max|w| * 2^e in [2^14, 2^15), so hi = fp16(v) and lo = fp16(v - hi) are both normal for every
+// weight within 2^17 of the layer's largest (|r| <= 2^-22 |v|; an unscaled 0.05 weight would leave lo
+// subnormal, ~2^-20) and nothing overflows.  The epilogues undo it on the fp32 accumulator with one
+// exact ldexp (ConvParams::wexp).  A layer of zeros keeps e = 0.
+__global__ void weight_absmax_kernel(const float* __restrict__ w, int64_t n, unsigned* __restrict__ out) {
   __shared__ float red[256];
-  const int co = blockIdx.x;
   float m = 0.0f;
-  for (int i = threadIdx.x; i < per_row; i += 256) m = fmaxf(m, fabsf(w[(int64_t)co * per_row + i]));
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, fabsf(w[i]));
   red[threadIdx.x] = m;
   __syncthreads();
   for (int k = 128; k > 0; k >>= 1) {
     if (threadIdx.x < k) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + k]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    int e = 0;
-    if (red[0] > 0.0f && isfinite(red[0])) {
-      int ex;
-      frexpf(red[0], &ex);  // max = f * 2^ex, f in [0.5, 1)  ->  max * 2^(15 - ex) in [2^14, 2^15)
-      e = min(max(15 - ex, -60), 60);
-    }
-    wscale[co] = ldexpf(1.0f, -e);
-  }
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(red[0]));  // non-negative floats order as uints
 }
 
-// weights [Cout][Cin][K][K] fp32 -> hi/lo fp16 [Cout][K*K][cin_pad] (zero padded), rows prescaled by
-// 1 / wscale[co] when wscale is given
+int weight_prescale_exp(const float* w, int64_t n, hipStream_t st) {
+  unsigned* d = nullptr;
+  HIP_OK(hipMalloc(&d, sizeof(unsigned)));
+  HIP_OK(hipMemsetAsync(d, 0, sizeof(unsigned), st));
+  const int nb = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(weight_absmax_kernel, dim3(std::max(1, nb)), dim3(256), 0, st, w, n, d);
+  unsigned u = 0;
+  HIP_OK(hipMemcpyAsync(&u, d, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipFree(d));
+  float m;
+  std::memcpy(&m, &u, sizeof m);
+  if (!(m > 0.0f) || !std::isfinite(m)) return 0;
+  int ex;
+  std::frexp(m, &ex);  // m = f * 2^ex, f in [0.5, 1)  ->  m * 2^(15 - ex) in [2^14, 2^15)
+  return std::min(std::max(15 - ex, -60), 60);
+}
+
+// weights [Cout][Cin][K][K] fp32 -> hi/lo fp16 [Cout][K*K][cin_pad] (zero padded) of w * 2^wexp
 __global__ void split_weights_kernel(const float* __restrict__ w, _Float16* __restrict__ wh, _Float16* __restrict__ wl,
-                                     int Cout, int Cin, int KK, int cin_pad, const float* __restrict__ wscale) {
+                                     int Cout, int Cin, int KK, int cin_pad, int wexp) {
   const int64_t n = (int64_t)Cout * KK * cin_pad;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int ci = (int)(i % cin_pad);
   const int tap = (int)((i / cin_pad) % KK);
   const int co = (int)(i / ((int64_t)cin_pad * KK));
-  float v = ci < Cin ? w[((int64_t)co * Cin + ci) * KK + tap] : 0.0f;
-  if (wscale) v = v / wscale[co];  // exact: a power of two
+  const float v = ci < Cin ? ldexpf(w[((int64_t)co * Cin + ci) * KK + tap], wexp) : 0.0f;
   const _Float16 h = (_Float16)v;
   wh[i] = h;
   wl[i] = (_Float16)(v - (float)h);
 }
 
-void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad, float* wscale,
-                   hipStream_t st) {
-  if (wscale) {
-    hipLaunchKernelGGL(weight_row_scale_kernel, dim3(Cout), dim3(256), 0, st, w, Cin * KK, wscale);
-    HIP_OK(hipGetLastError());
-  }
+int split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad, bool prescale,
+                  hipStream_t st) {
+  const int wexp = prescale ? weight_prescale_exp(w, (int64_t)Cout * Cin * KK, st) : 0;
   const int64_t n = (int64_t)Cout * KK * cin_pad;
   hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, wh, wl, Cout, Cin,
-                     KK, cin_pad, (const float*)wscale);
+                     KK, cin_pad, wexp);
   HIP_OK(hipGetLastError());
+  return wexp;
 }
 
 }  // namespace mlic

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
       dst[j] = square ? v * v : v;
     }
   };
+  bool bad = false;  // fp16 range guard (common.h)
   auto store_p = [&](int buf, int part, const float (&v8)[8]) {
     const int item = part * HT + tid;
     if (item >= G::PITEMS) return;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
     half8 h, l;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      range_check(P.rflag, v8[j]);
+      bad |= f16_unsafe(v8[j]);
       const _Float16 hv = (_Float16)v8[j];
       h[j] = hv;
       l[j] = (_Float16)(v8[j] - (float)hv);
@@ -241,6 +242,7 @@ __global__ __launch_bounds__(HT) void conv_halo_kernel(ConvParams P, const _Floa
     }
   }
 
+  range_report(P.rflag, bad);
   // ---- epilogue (C/D map: col = lane&31 = pixel column, row = Cout)
   const int khalf = lane >> 5;
 #pragma unroll

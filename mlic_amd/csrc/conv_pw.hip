@@ -59,10 +59,9 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
   constexpr int APITCH = pw_apitch<CIN>();
   constexpr int ROWS = CT * 32;
   constexpr int A_SZ = ROWS * APITCH;
-  static_assert(CIN % 16 == 0 && 2 * A_SZ * 2 + ROWS * 8 <= LDS_BYTES, "pw_resident: weights must fit in LDS");
-  __shared__ __attribute__((aligned(16))) _Float16 sm[2 * A_SZ + 4 * ROWS];  // + fp32 bias[ROWS], wscale[ROWS]
+  static_assert(CIN % 16 == 0 && 2 * A_SZ * 2 + ROWS * 4 <= LDS_BYTES, "pw_resident: weights must fit in LDS");
+  __shared__ __attribute__((aligned(16))) _Float16 sm[2 * A_SZ + 2 * ROWS];  // + fp32 bias[ROWS]
   float* sbias = reinterpret_cast<float*>(sm + 2 * A_SZ);
-  float* sscale = sbias + ROWS;
 
   const int tid = threadIdx.x;
   constexpr int QPR = CIN / 8;  // 16-byte chunks per weight row
@@ -76,10 +75,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
     *reinterpret_cast<uint4*>(sm + row * APITCH + 8 * q) = h;
     *reinterpret_cast<uint4*>(sm + A_SZ + row * APITCH + 8 * q) = l;
   }
-  for (int r = tid; r < ROWS; r += PW_THREADS) {
-    sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
-    sscale[r] = (P.wscale && r < P.Cout) ? P.wscale[r] : 1.0f;
-  }
+  for (int r = tid; r < ROWS; r += PW_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
   __syncthreads();
 
   const int lane = tid & 63;
@@ -126,6 +122,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
 
   const _Float16* Ah = sm + l32 * APITCH + 8 * h;
   const _Float16* Al = Ah + A_SZ;
+  bool bad = false;  // fp16 range guard (common.h)
   for (; tile < ntiles; tile += tstride) {
     int nt = tile + tstride;
     if (nt >= ntiles) nt = tile;  // last tile: reload the current one (keeps every load unconditional)
@@ -149,7 +146,6 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
       for (int i = 0; i < 8; ++i) {
         float v = ring[j % D][i];
         if (square) v *= v;
-        range_check(P.rflag, v);
         const _Float16 hv = (_Float16)v;
         bh[i] = hv;
         bl[i] = (_Float16)(v - (float)hv);
@@ -197,7 +193,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
     const uint32_t vo_aux = (uint32_t)p * 4u + (uint32_t)(4 * h) * ho4;
     const auto rs_res = make_rsrc(res ? P.res + (int64_t)b * P.res_bs : P.out, res ? (uint32_t)P.Cout * cs4 : 0u);
     const float* sb = sbias + 4 * h;  // per-lane base; the channel part folds into the ds_read offset
-    const float* ss = sscale + 4 * h;
+    const int wexp = P.wexp;
     // per co-tile: issue the 16 aux / residual loads together, then one wait, then 16 stores
     uint32_t so_o = 0, so_a = 0;  // channel byte offsets co_u * out_cs * 4 and co_u * HW * 4
     if (p < HW) {
@@ -225,8 +221,11 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
             oo += (((r & 3) == 0) ? 5u : 1u) * cs4;
             opaque(oo);
           }
-          float v = acc[c][r] * ss[c * 32 + (r & 3) + 8 * (r >> 2)];
+          float v = ldexpf(acc[c][r], -wexp);
           v += sb[c * 32 + (r & 3) + 8 * (r >> 2)];
+          // fp16 range guard on the accumulator (an input beyond fp16 splits to inf/NaN and poisons it;
+          // checked before GDN, whose rsqrt(inf) = 0 would hide it); cheaper here than in the ring
+          bad |= !(fabsf(v) <= 3.4e38f);
           if (gelu) v = gelu_erf(v);
           if (gdn) v = gdn_apply(xa[r], v, igdn);
           v += xr[r];
@@ -240,6 +239,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
       }
     }
   }
+  range_report(P.rflag, bad);
 }
 
 static int num_cus() {

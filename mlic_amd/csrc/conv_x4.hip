@@ -289,12 +289,13 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   const int64_t HW = Q.npix;  // channel plane stride of the (unfolded) input
   const float* src = sg.p + (int64_t)b * sg.bs + (int64_t)(ch0 - c0) * HW + (int64_t)y * Q.W + x;
   half8 h, l;
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const bool ok = inb && ch0 + j < Q.Cin && ch0 - c0 + j < sg.C;
     float v = ok ? src[(int64_t)j * HW] : 0.0f;
     if (Q.square) v *= v;
-    range_check(Q.rflag, v);
+    bad |= f16_unsafe(v);
     const _Float16 hv = (_Float16)v;
     h[j] = hv;
     l[j] = (_Float16)(v - (float)hv);
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   _Float16* d = Q.dst + (((int64_t)b * Q.nchunk + cc) * Hp * Wp + pos) * ROWH + 8 * g;
   *reinterpret_cast<half8*>(d) = h;
   *reinterpret_cast<half8*>(d + 32) = l;
+  range_report(Q.rflag, bad);
 }
 
 // weights: hi/lo [Cout][KK][cin_pad] -> [ct][step = chunk*KK + tap][BM rows][64 halves], swizzled

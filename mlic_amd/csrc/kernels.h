@@ -17,9 +17,10 @@ int conv_f16x3_variant(const ConvParams& P);
 void conv_f16x3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 int conv_x3v2_variant(const ConvParams& P);
 void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
-// wscale (optional, [Cout]): receives 2^-e of the exact per-row prescale applied before the split
-void split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad, float* wscale,
-                   hipStream_t st);
+// prescale: split w * 2^e with the layer's max |w| * 2^e in [2^14, 2^15); returns e (0 without
+// prescale).  Synchronises st.
+int split_weights(const float* w, _Float16* wh, _Float16* wl, int Cout, int Cin, int KK, int cin_pad, bool prescale,
+                  hipStream_t st);
 
 // specialised convs (conv_pw.hip)
 bool pw_resident_ok(const ConvParams& P, int cin_pad);
@@ -53,7 +54,7 @@ struct ConvWeights {
   const _Float16* wl;
   int cin_pad;
   const _Float16* wx4 = nullptr;  // x4_pack_weights image (null: CONV_X4 not available)
-  const float* ws = nullptr;      // per-row prescale of wh/wl (split_weights), applied by the split paths
+  int wexp = 0;                   // wh/wl hold w * 2^wexp (split_weights)
 };
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision);
 // device workspace conv_run needs for impl (bytes; 0 = none)
@@ -184,7 +185,7 @@ struct ChainParams {
   int nseg, cin0;  // layer-0 input: channel concat, cin0 % 32 == 0
   int HW, B;       // pixels per image (HW % 4 == 0)
   const float* bias[4];
-  const float* wscale[4];  // per-row prescale of each layer's split weights (split_weights), or null
+  int wexp[4];       // each layer's split weights are w * 2^wexp (split_weights)
   int gelu_mask;   // bit l: GELU after layer l (l < nl - 1)
   const _Float16* wimg;
   float* out;      // [B][cout[nl-1]][HW] (batch stride out_bs)

@@ -68,11 +68,11 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     total += ((size_t)e * 4 + 255) & ~(size_t)255;
   }
   for (int i = 0; i < n; ++i) {
-    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(2 * numel[i] + 2 * shapes[i * 4]) * 4 + 1280;
+    if (ends_with(names[i], ".gamma") && ndims[i] == 2) total += (size_t)(2 * numel[i] + shapes[i * 4]) * 4 + 1024;
     if (ends_with(names[i], ".weight") && (ndims[i] == 4 || ndims[i] == 2)) {
       // split fp16 copy: 2 x Cout x KK x cin_pad halves
       const int64_t cout = shapes[i * 4], per = numel[i] / std::max<int64_t>(1, cout);
-      total += (size_t)(cout * (per + 32 * 25)) * 4 + 1024 + (size_t)cout * 4 + 256;
+      total += (size_t)(cout * (per + 32 * 25)) * 4 + 1024;
     }
   }
   total += 64 * 4 + 625 * 4 + 1024;
@@ -131,8 +131,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
         const int64_t nh = (int64_t)w.Cout * w.K * w.K * w.cin_pad;
         w.wh = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
         w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
-        w.ws = take(w.Cout);
-        split_weights(ptrs[i], w.wh, w.wl, w.Cout, w.Cin, w.K * w.K, w.cin_pad, w.ws, st);
+        w.wexp = split_weights(ptrs[i], w.wh, w.wl, w.Cout, w.Cin, w.K * w.K, w.cin_pad, true, st);
       }
       w.name = base;
       convs_[base] = w;
@@ -173,9 +172,8 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     const int64_t nh = (int64_t)C * w.cin_pad;
     w.wh = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
     w.wl = reinterpret_cast<_Float16*>(take((nh + 1) / 2));
-    w.ws = take(C);
     MLIC_CHECK(off <= total, "weight block");
-    split_weights(gamma_eff, w.wh, w.wl, C, C, 1, w.cin_pad, w.ws, st);
+    w.wexp = split_weights(gamma_eff, w.wh, w.wl, C, C, 1, w.cin_pad, true, st);
     w.name = p + ".__gdn";
     convs_[p + ".__gdn"] = w;
   }
@@ -231,7 +229,7 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
       for (int cell = 0; cell < 25; ++cell) wp[(size_t)co * CIN + cell * 32 + c] = w[(size_t)co * CIN + c * 25 + cell];
   const int64_t nh = (int64_t)Cout * CIN, nx = x4_weight_halves(Cout, 1, CIN);
   char* blk = nullptr;
-  const size_t bytes = (size_t)nh * 4 + 2 * (size_t)nh * 2 + (size_t)nx * 2 + (size_t)Cout * 4 + 2048;
+  const size_t bytes = (size_t)nh * 4 + 2 * (size_t)nh * 2 + (size_t)nx * 2 + 1024;
   HIP_OK(hipMalloc(&blk, bytes));
   owned_.push_back(blk);
   wbytes_ += bytes;
@@ -239,9 +237,8 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
   _Float16* wh = reinterpret_cast<_Float16*>(blk + (size_t)nh * 4);
   _Float16* wl = wh + nh;
   _Float16* wx = reinterpret_cast<_Float16*>((reinterpret_cast<uintptr_t>(wl + nh) + 255) & ~(uintptr_t)255);
-  float* wsc = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(wx + nx) + 255) & ~(uintptr_t)255);
   HIP_OK(hipMemcpyAsync(wf, wp.data(), wp.size() * 4, hipMemcpyHostToDevice, st));
-  split_weights(wf, wh, wl, Cout, CIN, 1, CIN, wsc, st);
+  const int wexp = split_weights(wf, wh, wl, Cout, CIN, 1, CIN, true, st);
   x4_pack_weights(wh, wl, Cout, 1, CIN, wx, st);
   HIP_OK(hipStreamSynchronize(st));  // the host staging vectors die here
   ConvW cw;
@@ -253,7 +250,7 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
   cw.wl = wl;
   cw.cin_pad = CIN;
   cw.wx4 = wx;
-  cw.ws = wsc;
+  cw.wexp = wexp;
   cw.name = base;
   convs_[base + ".__x4perm"] = cw;
 }
@@ -285,7 +282,7 @@ void Model::add_chains(hipStream_t st) {
       const ConvW& w = it->second;
       c.cout[l] = w.Cout;
       c.bias[l] = w.b;
-      c.ws[l] = w.ws;
+      c.wexp[l] = w.wexp;
       if (l == 0) c.cin0 = w.Cin;
       else if (w.Cin != c.cout[l - 1]) ok = false;
       total += chain_layer_halves(w.Cout, w.Cin);
@@ -412,7 +409,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
                       const View& out2, int epi2) {
   const ConvParams P1 = conv_params(ins, w1, 1, w1.K / 2, out1, epi1, nullptr, nullptr);
   const ConvParams P2 = conv_params(ins, w2, 1, w2.K / 2, out2, epi2, nullptr, nullptr);
-  const ConvWeights c1{w1.w, w1.wh, w1.wl, w1.cin_pad, w1.wx4, w1.ws}, c2{w2.w, w2.wh, w2.wl, w2.cin_pad, w2.wx4, w2.ws};
+  const ConvWeights c1{w1.w, w1.wh, w1.wl, w1.cin_pad, w1.wx4, w1.wexp}, c2{w2.w, w2.wh, w2.wl, w2.cin_pad, w2.wx4, w2.wexp};
   if (conv_select(P1, c1, precision_) != CONV_X4 || conv_select(P2, c2, precision_) != CONV_X4 ||
       w1.cin_pad != w2.cin_pad || w1.K != w2.K) {
     run_conv(P1, w1, nullptr);
@@ -430,7 +427,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
 
 // packed: the input already in x4's split layout (conv_pair); the impl is then necessarily x4
 void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed) {
-  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4, w.ws};
+  const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4, w.wexp};
   const int impl = packed ? CONV_X4 : conv_select(P, cw, precision_);
   const double outn = (double)P.B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * P.Cin * w.K * w.K;
@@ -469,7 +466,7 @@ ConvParams Model::conv_params(const std::vector<View>& ins, const ConvW& w, int 
   P.Ho = (P.H + 2 * pad - w.K) / stride + 1;
   P.Wo = (P.W + 2 * pad - w.K) / stride + 1;
   P.wpk = w.w;
-  P.wscale = w.ws;  // conv_run clears it for the fp32 families
+  P.wexp = w.wexp;  // conv_run clears it for the fp32 families
   P.rflag = rflag_;
   P.bias = w.b;
   P.epi = epi;
@@ -540,7 +537,7 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   P.B = L().B;
   for (int l = 0; l < 4; ++l) {
     P.bias[l] = c.bias[l];
-    P.wscale[l] = c.ws[l];
+    P.wexp[l] = c.wexp[l];
   }
   P.gelu_mask = (1 << (c.nl - 1)) - 1;
   P.wimg = c.wimg;

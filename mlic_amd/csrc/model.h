@@ -32,7 +32,7 @@ struct ConvW {
   _Float16* wl = nullptr;
   int cin_pad = 0;
   _Float16* wx4 = nullptr;   // x4 LDS-image weights [ct][step][BM][64]     (conv_x4 path)
-  float* ws = nullptr;       // [Cout] 2^-e of the exact per-row prescale of wh/wl (split_weights)
+  int wexp = 0;              // wh/wl hold w * 2^wexp (exact layer prescale, split_weights)
   std::string name;          // state_dict prefix (profiling)
 };
 
@@ -42,7 +42,7 @@ struct ChainW {
   int nl = 0, cin0 = 0;
   int cout[4] = {0, 0, 0, 0};
   const float* bias[4] = {nullptr, nullptr, nullptr, nullptr};
-  const float* ws[4] = {nullptr, nullptr, nullptr, nullptr};
+  int wexp[4] = {0, 0, 0, 0};
   std::string name;
 };
 
