@@ -195,9 +195,23 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 
   // ------------------------------------------------------------------ layer 0 (input prefetched)
   floatx4 acc0[C1 / 16][2];
+  if (P.aux) {
+    // the hoisted part of layer 0 (EntropyParameters' hyper columns, one wide GEMM per image) starts
+    // the accumulators, in the prescaled domain of this layer's weights (exact)
+    const float* ax = P.aux + (int64_t)b * P.aux_bs;
 #pragma unroll
-  for (int i = 0; i < C1 / 16; ++i)
-    for (int j = 0; j < 2; ++j) acc0[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) {
+      const int px = min(p0 + 32 * wv + 16 * j + l16, HW - 1);
+#pragma unroll
+      for (int i = 0; i < C1 / 16; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc0[i][j][e] = ldexpf(ax[(int64_t)(16 * i + 4 * G + e) * HW + px], P.wexp[0]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < C1 / 16; ++i)
+      for (int j = 0; j < 2; ++j) acc0[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
   auto step0 = [&](int t, float (&f)[2][8]) {
     if (t >= S0) return;
     step_begin(t);
@@ -331,7 +345,8 @@ bool chain_supported(int nl, const int* cout) {
 
 void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st) {
   MLIC_CHECK(chain_supported(nl, cout), "chain: unsupported layer widths");
-  MLIC_CHECK(P.cin0 % 32 == 0 && P.cin0 > 0 && P.HW % 4 == 0 && P.HW >= 4, "chain: Cin multiple of 32, HW of 4");
+  MLIC_CHECK(P.cin0 % 32 == 0 && (P.cin0 > 0 || P.aux) && P.HW % 4 == 0 && P.HW >= 4,
+             "chain: Cin multiple of 32 (or 0 with aux), HW of 4");
   dim3 grid((P.HW + CH_BN - 1) / CH_BN, P.B);
   if (nl == 4 && cout[3] == 64)
     hipLaunchKernelGGL((chain_kernel<320, 256, 128, 64>), grid, dim3(CH_T), 0, st, P);

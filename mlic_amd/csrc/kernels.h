@@ -193,6 +193,8 @@ struct ChainParams {
   const float* res;  // optional residual added to the output (same layout, batch stride res_bs)
   int64_t res_bs;
   int* rflag;        // fp16 range guard (common.h range_check)
+  const float* aux;  // optional [B][C1][HW] added to layer 0's pre-activation (hoisted part of layer 0)
+  int64_t aux_bs;
 };
 bool chain_supported(int nl, const int* cout);
 int64_t chain_layer_halves(int Cout, int Cin);

@@ -93,9 +93,12 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
   for (int i = 0; i < n; ++i) idx[names[i]] = i;
   auto shape = [&](int i, int d) { return (int)shapes[i * 4 + d]; };
 
+  std::map<std::string, std::pair<const float*, int>> ep0;  // EntropyParameters layer-0 weights (hoisting)
   for (int i = 0; i < n; ++i) {
     const std::string k = names[i];
     float* dst = take(numel[i]);
+    if (k.rfind("entropy_parameters", 0) == 0 && ends_with(k, ".fusion.0.weight") && ndims[i] == 4)
+      ep0[k.substr(0, k.size() - 9)] = {ptrs[i], shape(i, 1)};
     const std::string base = k.substr(0, k.rfind('.'));
     if (ends_with(k, ".weight") && ndims[i] == 4 && shape(i, 1) == 1 && shape(i, 0) > 1) {
       // depthwise [C,1,3,3]
@@ -212,6 +215,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     HIP_OK(hipMemcpyAsync(rel_index_, ri.data(), ri.size() * 4, hipMemcpyHostToDevice, st));
   }
   add_chains(st);
+  add_hoist(ep0, st);
   MLIC_CHECK(raw_.count("__scale_table"), "scale table missing");
   scale_table_ = const_cast<float*>(raw_["__scale_table"]);
   HIP_OK(hipStreamSynchronize(st));
@@ -269,6 +273,7 @@ void Model::add_chains(hipStream_t st) {
       todo.push_back({p, {p + ".fc1", p + ".fc2"}});
     }
   }
+  const int hyp = 2 * cfg_.hM();  // hyper_params channels: the last segment of every EP input
   int64_t total = 0;
   std::vector<ChainW> cws;
   for (auto& t : todo) {
@@ -287,7 +292,17 @@ void Model::add_chains(hipStream_t st) {
       else if (w.Cin != c.cout[l - 1]) ok = false;
       total += chain_layer_halves(w.Cout, w.Cin);
     }
-    if (ok && chain_supported(c.nl, c.cout) && c.cin0 % 32 == 0) cws.push_back(c);
+    if (ok && chain_supported(c.nl, c.cout) && c.cin0 % 32 == 0) {
+      cws.push_back(c);
+      if (c.nl == 4 && c.cin0 >= hyp && (c.cin0 - hyp) % 32 == 0) {  // the hoisted variant: context columns
+        ChainW h = c;
+        h.cin0 = c.cin0 - hyp;
+        h.name = c.name + "#ctx";
+        total += chain_layer_halves(c.cout[0], h.cin0);
+        for (int l = 1; l < c.nl; ++l) total += chain_layer_halves(c.cout[l], c.cout[l - 1]);
+        cws.push_back(h);
+      }
+    }
   }
   if (cws.empty()) return;
   _Float16* blk = nullptr;
@@ -297,15 +312,84 @@ void Model::add_chains(hipStream_t st) {
   int64_t off = 0;
   for (ChainW& c : cws) {
     c.wimg = blk + off;
-    const auto& names = c.nl == 4 ? std::vector<std::string>{c.name + ".0", c.name + ".2", c.name + ".4", c.name + ".6"}
-                                  : std::vector<std::string>{c.name + ".fc1", c.name + ".fc2"};
+    const bool ctx = ends_with(c.name, "#ctx");
+    const std::string base = ctx ? c.name.substr(0, c.name.size() - 4) : c.name;
+    const auto& names = c.nl == 4 ? std::vector<std::string>{base + ".0", base + ".2", base + ".4", base + ".6"}
+                                  : std::vector<std::string>{base + ".fc1", base + ".fc2"};
     for (int l = 0; l < c.nl; ++l) {
       const ConvW& w = convs_.at(names[l]);
-      chain_pack(w.wh, w.wl, w.Cout, w.Cin, w.cin_pad, l > 0 ? 1 : 0, blk + off, st);
-      off += chain_layer_halves(w.Cout, w.Cin);
+      const int cin = l == 0 ? c.cin0 : w.Cin;  // the hoisted variant packs the leading (context) columns
+      if (cin > 0) chain_pack(w.wh, w.wl, w.Cout, cin, w.cin_pad, l > 0 ? 1 : 0, blk + off, st);
+      off += chain_layer_halves(w.Cout, cin);
     }
-    chains_[c.name] = c;
+    if (ctx) {
+      c.name = base;
+      chains_ctx_[base] = c;
+    } else {
+      chains_[c.name] = c;
+    }
   }
+}
+
+// a standalone conv weight (the model's layer weights come from the state_dict loop above)
+ConvW Model::make_conv(const float* w_dev, int Cout, int Cin, int K, const std::string& name, hipStream_t st) {
+  ConvW w;
+  w.Cout = Cout;
+  w.Cin = Cin;
+  w.K = K;
+  w.cin_pad = (Cin + 31) / 32 * 32;
+  w.name = name;
+  const int64_t nw = (int64_t)Cout * Cin * K * K, nh = (int64_t)Cout * K * K * w.cin_pad;
+  const int64_t nx = (K == 1 || K == 3 || K == 5) && Cout >= 64 ? x4_weight_halves(Cout, K * K, w.cin_pad) : 0;
+  const size_t bytes = ((size_t)nw * 4 + 255) / 256 * 256 + 2 * (((size_t)nh * 2 + 255) / 256 * 256) + (size_t)nx * 2 + 256;
+  char* blk = nullptr;
+  HIP_OK(hipMalloc(&blk, bytes));
+  owned_.push_back(blk);
+  wbytes_ += bytes;
+  w.w = reinterpret_cast<float*>(blk);
+  w.wh = reinterpret_cast<_Float16*>(blk + ((size_t)nw * 4 + 255) / 256 * 256);
+  w.wl = w.wh + ((size_t)nh * 2 + 255) / 256 * 256 / 2;
+  pack_conv(w_dev, w.w, Cout, Cin, K * K, st);
+  w.wexp = split_weights(w_dev, w.wh, w.wl, Cout, Cin, K * K, w.cin_pad, true, st);
+  if (nx) {
+    w.wx4 = w.wl + ((size_t)nh * 2 + 255) / 256 * 256 / 2;
+    x4_pack_weights(w.wh, w.wl, Cout, K * K, w.cin_pad, w.wx4, st);
+  }
+  return w;
+}
+
+// EntropyParameters' layer 0 over [context..., hyper_params]: the hyper columns of all 2 S EPs stacked
+// into one [2 S x C1][2 hM] weight (slot 2 i + nonanchor), so W_hyp . hyper is one GEMM per image
+void Model::add_hoist(const std::map<std::string, std::pair<const float*, int>>& ep0, hipStream_t st) {
+  const int hyp = 2 * cfg_.hM(), S = cfg_.S;
+  if ((int)ep0.size() != 2 * S || chains_ctx_.size() != (size_t)(2 * S)) return;
+  const int C1 = convs_.at("entropy_parameters_anchor.0.fusion.0").Cout;
+  float* tmp = nullptr;
+  HIP_OK(hipMalloc(&tmp, sizeof(float) * (size_t)2 * S * C1 * hyp));
+  for (int i = 0; i < S; ++i)
+    for (int k = 0; k < 2; ++k) {
+      const std::string p = std::string("entropy_parameters_") + (k ? "nonanchor." : "anchor.") + std::to_string(i) +
+                            ".fusion.0";
+      auto it = ep0.find(p);
+      MLIC_CHECK(it != ep0.end() && convs_.at(p).Cout == C1, "hoist: EP layer 0");
+      const float* src = it->second.first;
+      const int cin = it->second.second;
+      HIP_OK(hipMemcpy2DAsync(tmp + (size_t)(2 * i + k) * C1 * hyp, (size_t)hyp * 4, src + (cin - hyp), (size_t)cin * 4,
+                              (size_t)hyp * 4, C1, hipMemcpyDeviceToDevice, st));
+    }
+  hoist_ = make_conv(tmp, 2 * S * C1, hyp, 1, "__hyper_hoist", st);
+  hoist_rows_ = C1;
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipFree(tmp));
+}
+
+// $MLIC_HOIST=0: EntropyParameters consume hyper_params inside each chain (A/B switch)
+bool Model::hoist_on() const {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_HOIST");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && chain_on() && hoist_.Cout > 0;
 }
 
 // $MLIC_CHAIN=0: the per-layer path for EntropyParameters / LocalContext MLP (A/B switch)
@@ -520,20 +604,30 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
 }
 
 // a fused chain over a (multi-segment) input; GELU between the layers (entropy.py:10-18, MLP fc1 -> fc2)
-void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res) {
+void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
+                      const View* aux, int H, int W) {
   ChainParams P{};
-  MLIC_CHECK(!ins.empty() && (int)ins.size() <= MAXSEG, "chain inputs");
+  MLIC_CHECK((int)ins.size() <= MAXSEG && (!ins.empty() || aux), "chain inputs");
+  if (!ins.empty()) {
+    H = ins[0].H;
+    W = ins[0].W;
+  }
   P.nseg = (int)ins.size();
   int cin = 0;
   for (int s = 0; s < P.nseg; ++s) {
-    MLIC_CHECK(ins[s].H == ins[0].H && ins[s].W == ins[0].W, "chain inputs must share H, W");
+    MLIC_CHECK(ins[s].H == H && ins[s].W == W, "chain inputs must share H, W");
     P.seg[s] = {ins[s].p, ins[s].C, ins[s].bs};
     cin += ins[s].C;
   }
   MLIC_CHECK(cin == c.cin0, "chain Cin mismatch");
-  MLIC_CHECK(out.C == c.cout[c.nl - 1] && out.H == ins[0].H && out.W == ins[0].W, "chain output shape");
+  MLIC_CHECK(out.C == c.cout[c.nl - 1] && out.H == H && out.W == W, "chain output shape");
+  if (aux) {
+    MLIC_CHECK(aux->C == c.cout[0] && aux->H == H && aux->W == W, "chain aux shape");
+    P.aux = aux->p;
+    P.aux_bs = aux->bs;
+  }
   P.cin0 = cin;
-  P.HW = ins[0].H * ins[0].W;
+  P.HW = H * W;
   P.B = L().B;
   for (int l = 0; l < 4; ++l) {
     P.bias[l] = c.bias[l];
@@ -552,7 +646,7 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   double mac = (double)c.cin0 * c.cout[0];
   for (int l = 1; l < c.nl; ++l) mac += (double)c.cout[l - 1] * c.cout[l];
   const double pix = (double)P.B * P.HW;
-  const double bytes = 4.0 * (pix * (cin + out.C * (res ? 2 : 1)) + mac);
+  const double bytes = 4.0 * (pix * (cin + out.C * (res ? 2 : 1) + (aux ? c.cout[0] : 0)) + mac);
   timed(PCAT_CHAIN, 2.0 * mac * pix, bytes, [&] { chain_forward(P, c.nl, c.cout, L().st); }, c.name);
 }
 
@@ -879,11 +973,22 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
 }
 
 // entropy.py:7-29
-View Model::entropy_parameters(const std::vector<View>& ins, const std::string& kind, int i) {
+View Model::entropy_parameters(const std::vector<View>& ctx, const View* hyper, const std::string& kind, int i,
+                               const View* hoisted) {
   const std::string p = "entropy_parameters_" + kind + "." + std::to_string(i) + ".fusion";
-  const int H = ins[0].H, W = ins[0].W;
+  const View& geo = ctx.empty() ? *hyper : ctx[0];
+  const int H = geo.H, W = geo.W;
   const ConvW& l3 = cw(p + ".6");
   View out = alloc(l3.Cout, H, W);
+  auto hc = chains_ctx_.find(p);
+  if (hoisted && hc != chains_ctx_.end() && (H * W) % 4 == 0) {
+    const int slot = 2 * i + (kind == "nonanchor" ? 1 : 0);
+    const View aux = hoisted->ch(slot * hoist_rows_, hoist_rows_);
+    run_chain(hc->second, ctx, out, nullptr, &aux, H, W);
+    return out;
+  }
+  std::vector<View> ins = ctx;
+  if (hyper) ins.push_back(*hyper);
   auto ch = chains_.find(p);
   if (chain_on() && ch != chains_.end() && (H * W) % 4 == 0) {
     run_chain(ch->second, ins, out, nullptr);
@@ -960,6 +1065,13 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
   const int H = hyper.H, W = hyper.W, HW = H * W;
   const int64_t n_per = (int64_t)C * H * (W / 2);
   const View hyper_means = hyper.ch(hM, hM);
+  View hoisted;  // W_hyp . hyper of all 2 S EntropyParameters (one GEMM, before the serial loop)
+  const View* hp = nullptr;
+  if (hoist_on() && HW % 4 == 0) {
+    hoisted = alloc(hoist_.Cout, H, W);
+    conv({hyper}, hoist_, 1, 0, hoisted, EPI_NONE);
+    hp = &hoisted;
+  }
   float* vbr_dev = nullptr;  // per-image VBR gains [2][B] (gain, 1 / gain)
   if (L().vbr_on) {
     MLIC_CHECK((int)L().vbr_host.size() == 2 * L().B, "vbr scales");
@@ -972,12 +1084,12 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
     View ysl = yhat.ch(idx * C, C);
     View inter, chan, pa;
     if (idx == 0) {
-      pa = entropy_parameters({hyper}, "anchor", 0);
+      pa = entropy_parameters({}, &hyper, "anchor", 0, hp);
     } else {
       View prev = yhat.ch(0, idx * C);
       inter = inter_context(prev, idx);
       chan = channel_context(prev, idx);
-      pa = entropy_parameters({inter, chan, hyper}, "anchor", idx);
+      pa = entropy_parameters({inter, chan}, &hyper, "anchor", idx, hp);
     }
     for (int ph = 0; ph < 2; ++ph) {
       QuantParams Q{};
@@ -997,10 +1109,10 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       if (ph == 1) {
         View local = local_context(ysl, idx);
         if (idx == 0) {
-          pn = entropy_parameters({local, hyper}, "nonanchor", 0);
+          pn = entropy_parameters({local}, &hyper, "nonanchor", 0, hp);
         } else {
           View intra = intra_context(yhat.ch((idx - 1) * C, C), ysl, idx);
-          pn = entropy_parameters({local, intra, inter, chan, hyper}, "nonanchor", idx);
+          pn = entropy_parameters({local, intra, inter, chan}, &hyper, "nonanchor", idx, hp);
         }
       }
       const View& par = ph == 0 ? pa : pn;
@@ -1456,8 +1568,8 @@ void Model::run_module(const std::string& which, int i, const float* in0, const 
     else if (which == "intra") {
       View b{const_cast<float*>(in1), Cin, H, W, (int64_t)Cin * H * W};
       r = intra_context(a, b, i);
-    } else if (which == "epa") r = entropy_parameters({a}, "anchor", i);
-    else if (which == "epn") r = entropy_parameters({a}, "nonanchor", i);
+    } else if (which == "epa") r = entropy_parameters({a}, nullptr, "anchor", i);
+    else if (which == "epn") r = entropy_parameters({a}, nullptr, "nonanchor", i);
     else if (which == "g_a") r = g_a(a);
     else if (which == "h_a") r = h_a(a);
     else if (which == "h_s") r = h_s(a);

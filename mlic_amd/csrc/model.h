@@ -170,11 +170,21 @@ class Model {
   Cfg cfg_;
   std::map<std::string, ConvW> convs_;
   std::map<std::string, ChainW> chains_;  // keyed by the module prefix (".fusion" / ".mlp")
+  // EntropyParameters with the hyper columns of layer 0 hoisted out of the slice loop: one GEMM
+  // W_hyp (all 2 S EPs stacked, 2 S x 320 rows) . hyper per image before the loop; the chains_ctx_
+  // then run layer 0 over the context channels only and start from the hoisted rows (aux)
+  std::map<std::string, ChainW> chains_ctx_;
+  ConvW hoist_;          // stacked [2 S x C1][2 hM] (Cout = 0: no hoisting)
+  int hoist_rows_ = 0;   // C1 (320)
+  bool hoist_on() const;
+  void add_hoist(const std::map<std::string, std::pair<const float*, int>>& ep0, hipStream_t st);
+  ConvW make_conv(const float* w_dev, int Cout, int Cin, int K, const std::string& name, hipStream_t st);
   void add_chains(hipStream_t st);
   int* rflag_ = nullptr;  // device fp16 range flag (common.h range_check)
   bool range_hit(hipStream_t st);
   void range_fail(hipStream_t st);
-  void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res);
+  void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
+                 const View* aux = nullptr, int H = 0, int W = 0);
   bool chain_on() const;
   std::map<std::string, DwW> dws_;
   std::map<std::string, const float*> raw_;
@@ -234,7 +244,10 @@ class Model {
   View channel_context(const View& x, int i);
   View inter_context(const View& x, int i);
   View intra_context(const View& x1, const View& x2, int i);
-  View entropy_parameters(const std::vector<View>& ins, const std::string& kind, int i);
+  // ctx: the context segments of the layer-0 concat (entropy.py), hyper appended last; hoisted: the
+  // slice loop's precomputed W_hyp . hyper rows of all EPs (or null)
+  View entropy_parameters(const std::vector<View>& ctx, const View* hyper, const std::string& kind, int i,
+                          const View* hoisted = nullptr);
   void lrp(const std::vector<View>& ins, const std::string& kind, int i, const View& yh_slice, bool anchor);
   View qkv_branch(const View& x, const std::string& p);
   void slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, int32_t* d_sym,
