@@ -98,7 +98,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     const std::string k = names[i];
     float* dst = take(numel[i]);
     if (k.rfind("entropy_parameters", 0) == 0 && ends_with(k, ".fusion.0.weight") && ndims[i] == 4)
-      ep0[k.substr(0, k.size() - 9)] = {ptrs[i], shape(i, 1)};
+      ep0[k.substr(0, k.size() - 7)] = {ptrs[i], shape(i, 1)};
     const std::string base = k.substr(0, k.rfind('.'));
     if (ends_with(k, ".weight") && ndims[i] == 4 && shape(i, 1) == 1 && shape(i, 0) > 1) {
       // depthwise [C,1,3,3]
