@@ -12,16 +12,17 @@
 //     rows 4*(lane>>4)+e of column lane&15, and two such blocks (rows 32c+{0..15} and 32c+{16..31})
 //     give lane group G = lane>>4 the 8 k-slots 8G..8G+7 of K-chunk c under the fixed permutation
 //     slot s -> row 16*((s>>2)&1) + 4*(s>>3) + (s&3).  The next layer's weights are packed with that
-//     K permutation, so bias + GELU + the hi/lo split happen in registers and nothing is staged;
-//   * weights stream through LDS: one K-step = 32 input channels x all output rows of the layer,
-//     pre-packed on the host side into the exact LDS image (128-byte rows: hi of 32 k | lo of 32 k,
-//     16-byte granule G of row n at G ^ ((n >> 1) & 7): conflict-free ds_read_b128 fragments), moved
-//     by global_load_lds_dwordx4 (LDS-DMA) into a 3-slot ring, two steps ahead;
+//     K permutation, so bias + GELU + the hi/lo split happen in registers and nothing is staged; the
+//     operands of K-chunk c + 1 are made while chunk c's MFMAs run (program-order interleave);
+//   * weights: one K-step = 32 input channels x all output rows of the layer, pre-packed on the host
+//     side into the exact LDS image (128-byte rows: hi of 32 k | lo of 32 k, 16-byte granule G of row
+//     n at G ^ ((n >> 1) & 7): conflict-free ds_read_b128 fragments).  Staged through registers
+//     (global_load_dwordx4, 1 KB per wave-instruction, L2-resident) one step ahead and stored with
+//     ds_write_b128 into a 2-slot LDS ring: measured far cheaper to issue next to the MFMA/ds_read
+//     stream than LDS-DMA pieces (tools/gpu/chain_probe.hip);
 //   * layer 0's input (fp32 NCHW, a multi-segment channel concat) is loaded by each lane straight into
-//     its B-fragment registers, three K-steps ahead (HBM latency), and split in registers;
-//   * the K-step sequence of all layers is one pipeline: one counted `s_waitcnt vmcnt` (weights of
-//     this step landed; the younger input loads and weight DMAs stay in flight) and one raw s_barrier
-//     per step.
+//     its B-fragment registers two K-steps ahead (a 2-deep register ring) and split in registers;
+//   * one s_barrier per K-step; every global load is compiler-visible (its vmcnt is the compiler's).
 #include "common.h"
 #include "kernels.h"
 
@@ -33,57 +34,61 @@ namespace mlic {
 namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int CH_T = 256;      // threads (4 waves)
 constexpr int CH_BN = 128;     // pixels per workgroup
 
 __device__ __forceinline__ int chswz(int row) { return (row >> 1) & 7; }
 
-__device__ __forceinline__ void chain_glds(const void* src, const void* lds) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane(
-      (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)lds));
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(l) : "m0");
-}
-
 __device__ __forceinline__ half8 chain_frag(const char* base, int row, int granule) {
   return *reinterpret_cast<const half8*>(base + row * 128 + ((granule ^ chswz(row)) << 4));
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (over-waits for n outside the cases)
-__device__ __forceinline__ void chain_wait(int n) {
-  switch (n) {
-#define MLIC_CW(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MLIC_CW(1) MLIC_CW(2) MLIC_CW(3) MLIC_CW(4) MLIC_CW(5) MLIC_CW(6) MLIC_CW(7) MLIC_CW(8) MLIC_CW(9)
-    MLIC_CW(10) MLIC_CW(11) MLIC_CW(12) MLIC_CW(13) MLIC_CW(14) MLIC_CW(15) MLIC_CW(16)
-#undef MLIC_CW
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l, bool& bad) {
+// hi/lo split of 8 values; bad: the fp16 range guard's per-lane bit (any |v| >= 65520, which rounds
+// to inf in fp16; a NaN propagates as on the fp32 path), pinned after every split (an asm operand) so
+// the compiler cannot sink the checks to the end of the kernel and keep every split value alive
+__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l, int& bad) {
+  float m = 0.0f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    bad |= f16_unsafe(v[e]);
+    m = __builtin_fmaxf(m, __builtin_fabsf(v[e]));
     const _Float16 hv = (_Float16)v[e];
     h[e] = hv;
     l[e] = (_Float16)(v[e] - (float)hv);
   }
+  bad |= m >= 65520.0f ? 1 : 0;
+  asm volatile("" : "+v"(bad));
 }
 }  // namespace
+
+#ifdef MLIC_CHAIN_TRACE
+// step timestamps of two workgroups (tools/gpu/chain_probe.hip): [wg][wave][step][3] shader clocks
+__device__ unsigned long long* g_chain_trace;
+constexpr int CH_TR_STEPS = 64;
+#endif
 
 template <int C1, int C2, int C3, int C4>
 __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   constexpr int NL = C4 ? 4 : (C3 ? 3 : 2);
-  constexpr int CMAX = C1;  // layer 0 is the widest (checked by the host side)
-  constexpr int WSLOT = CMAX * 128;
-  constexpr int B_OFF = 3 * WSLOT;
+  constexpr int WSLOT = C1 * 128;  // layer 0 is the widest (checked by the host side)
+  constexpr int B_OFF = 2 * WSLOT;
   constexpr int NB = C1 + C2 + C3 + C4;
-  static_assert(C1 % 32 == 0 && C2 % 16 == 0 && (C3 == 0 || C3 % 16 == 0) && (C4 == 0 || C4 % 16 == 0), "dims");
+  constexpr int WMAX = C1 / 32;  // 1-KB weight pieces per wave of the widest step
+  static_assert(C1 % 32 == 0 && C2 % 32 == 0 && (C3 == 0 || C3 % 32 == 0) && (C4 == 0 || C4 % 16 == 0), "dims");
+  static_assert(C2 <= C1 && C3 <= C1 && C4 <= C1, "layer 0 is the widest");
   static_assert(B_OFF + NB * 4 <= 160 * 1024, "chain LDS");
-  static_assert(NL == 2 || C2 % 32 == 0, "inner layers feed whole K chunks");
   __shared__ __attribute__((aligned(1024))) char sm[B_OFF + NB * 4];
   float* sbias = reinterpret_cast<float*>(sm + B_OFF);
+#ifdef MLIC_CHAIN_TRACE
+  __shared__ unsigned long long str[4][CH_TR_STEPS][3];
+  const int tr_wg = (blockIdx.x == 0 && blockIdx.y == 0) ? 0
+                    : (blockIdx.x == gridDim.x - 2 && blockIdx.y == gridDim.y - 1) ? 1 : -1;
+#define CH_TR(t, k) \
+  if (tr_wg >= 0 && (t) < CH_TR_STEPS) str[threadIdx.x >> 6][t][k] = __builtin_readcyclecounter()
+#else
+#define CH_TR(t, k)
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = lane >> 4, l16 = lane & 15;
@@ -94,7 +99,6 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   constexpr int S1 = C1 / 32, S2 = C2 / 32, S3 = C3 / 32;
   const int T = S0 + S1 + (NL > 2 ? S2 : 0) + (NL > 3 ? S3 : 0);
 
-  // biases to LDS (before any DMA: the loop below must see no compiler-visible global load)
   {
     constexpr int CS[4] = {C1, C2, C3, C4};
     int off = 0;
@@ -117,30 +121,43 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     return C4;
   };
 
-  // weight DMA: step w_next -> slot w_next % 3; each wave moves rows/32 KB-sized pieces
-  int w_next = 0;
-  int64_t w_off = 0;  // halves
-  auto issue_w = [&]() {
-    const int R = rows_of(w_next);
-    const int n = R / 32;
-    char* dst = sm + (w_next % 3) * WSLOT;
-    const _Float16* src = P.wimg + w_off + lane * 8;
-    for (int i = 0; i < n; ++i) {
-      const int ci = wv * n + i;
-      chain_glds(src + (int64_t)ci * 512, dst + ci * 1024);
-    }
+  // weights of step u: wave wv moves 1-KB pieces wv*n .. wv*n + n - 1 (n = rows / 32) through wr
+  u32x4 wr[WMAX];
+  int64_t w_off = 0;  // halves: the image of the next step to load
+  auto wload = [&](int u) {
+    const int R = rows_of(u), n = R / 32;
+    const _Float16* src = P.wimg + w_off + (int64_t)(wv * n) * 512 + lane * 8;
+#pragma unroll
+    for (int i = 0; i < WMAX; ++i)
+      if (i < n) wr[i] = *reinterpret_cast<const u32x4*>(src + i * 512);
     w_off += (int64_t)R * 64;
-    ++w_next;
   };
-  // layer-0 input: prefetched into registers 3 K-steps ahead (a 3-deep register ring, the loop below
-  // is unrolled by 3 so the ring index is static).  Lane (G, l16) loads exactly its B fragments:
+  auto wstore = [&](int u) {
+    const int n = rows_of(u) / 32;
+    char* dst = sm + (u & 1) * WSLOT + (wv * n) * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < WMAX; ++i)
+      if (i < n) *reinterpret_cast<u32x4*>(dst + i * 1024) = wr[i];
+  };
+  // top of step t: this wave's stores of W(t) done, then the barrier (W(t) visible to all waves; slot
+  // (t + 1) & 1, read in step t - 1, free); then W(t + 1) registers -> LDS and W(t + 2) -> registers
+  auto step_begin = [&](int t) {
+    CH_TR(t, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    CH_TR(t, 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    CH_TR(t, 2);
+    if (t + 1 < T) wstore(t + 1);
+    if (t + 2 < T) wload(t + 2);
+  };
+
+  // layer-0 input, 2 K-steps ahead in registers: lane (G, l16) loads exactly its B fragments,
   // channels 32t + 8G .. +7 at pixels p0 + 32 wv + 16 j + l16 (16 dword loads; the 32 channels of a
-  // K-step lie in one input segment, segments being multiples of 32).  These loads are compiler-
-  // visible: the compiler's own vmcnt for them only over-waits (it does not see the DMAs), and the
-  // explicit per-step wait below counts them (NF per step).
-  constexpr int NF = 16;
+  // K-step lie in one input segment, segments being multiples of 32).  Every L0 step issues its 16
+  // loads (the last two re-load chunk S0 - 1), so the ring's vmcnt stays a plain count.
   auto load_f = [&](int t, float (&f)[2][8]) {
-    if (t >= S0) return;
+    t = min(t, S0 - 1);
     const int ch = 32 * t;
     int s = 0, c0 = 0;
     while (s + 1 < P.nseg && ch >= c0 + P.seg[s].C) { c0 += P.seg[s].C; ++s; }
@@ -152,47 +169,37 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
       for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HW + px];
     }
   };
-  auto nf_of = [&](int t) { return t < S0 ? NF : 0; };
-  // at the top of step u only W(u) must have landed; issued after it: F(u+1), W(u+1), F(u+2)
-  auto step_begin = [&](int t) {
-    chain_wait(nf_of(t + 1) + rows_of(t + 1) / 32 + nf_of(t + 2));
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + 2 < T) issue_w();
-  };
 
   auto mfma3 = [](floatx4& acc, const half8& ah, const half8& al, const half8& bh, const half8& bl) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
   };
-  // one K-step of COUT rows against B operands in registers; the A fragments of row block i + 1 are
-  // read while block i's MFMAs issue
-  auto kstep = [&](auto& acc, const char* As, const half8 (&bh)[2], const half8 (&bl)[2], auto cout_c) {
-    constexpr int COUT = decltype(cout_c)::value;
-    half8 ah[2], al[2];
-    ah[0] = chain_frag(As, l16, G);
-    al[0] = chain_frag(As, l16, G + 4);
+  // one K-step of COUT rows against B operands in registers; the A fragments of row block i + 2 are
+  // read while block i's MFMAs issue (12 MFMAs of cover for the LDS latency); hook(i) runs after
+  // block i's MFMAs (program-order interleave of independent VALU work)
+  auto kstep = [&](auto& acc, const char* As, const half8 (&bh)[2], const half8 (&bl)[2], auto cout_c, auto&& hook) {
+    constexpr int COUT = decltype(cout_c)::value, NBK = COUT / 16, D = 2, R = D + 1;
+    half8 ah[R], al[R];
 #pragma unroll
-    for (int i = 0; i < COUT / 16; ++i) {
-      if (i + 1 < COUT / 16) {
-        ah[(i + 1) & 1] = chain_frag(As, 16 * (i + 1) + l16, G);
-        al[(i + 1) & 1] = chain_frag(As, 16 * (i + 1) + l16, G + 4);
+    for (int i = 0; i < D && i < NBK; ++i) {
+      ah[i] = chain_frag(As, 16 * i + l16, G);
+      al[i] = chain_frag(As, 16 * i + l16, G + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < NBK; ++i) {
+      if (i + D < NBK) {
+        ah[(i + D) % R] = chain_frag(As, 16 * (i + D) + l16, G);
+        al[(i + D) % R] = chain_frag(As, 16 * (i + D) + l16, G + 4);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) mfma3(acc[i][j], ah[i & 1], al[i & 1], bh[j], bl[j]);
+      for (int j = 0; j < 2; ++j) mfma3(acc[i][j], ah[i % R], al[i % R], bh[j], bl[j]);
+      hook(i);
     }
   };
+  auto no_hook = [](int) {};
 
-  bool bad = false;  // fp16 range guard (common.h)
-  // prologue, issued in the per-step order (step u issues W(u+2), then F(u+3)): F(0) W(0) F(1) W(1) F(2)
-  float fr[3][2][8];
-  load_f(0, fr[0]);
-  issue_w();
-  load_f(1, fr[1]);
-  if (T > 1) issue_w();
-  load_f(2, fr[2]);
-
+  int bad = 0;  // fp16 range guard (common.h)
   // ------------------------------------------------------------------ layer 0 (input prefetched)
   floatx4 acc0[C1 / 16][2];
   if (P.aux) {
@@ -213,62 +220,86 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
       for (int j = 0; j < 2; ++j) acc0[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
   auto step0 = [&](int t, float (&f)[2][8]) {
-    if (t >= S0) return;
     step_begin(t);
     half8 bh[2], bl[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) split8(f[j], bh[j], bl[j], bad);
-    load_f(t + 3, f);  // the ring slot is free once split
-    kstep(acc0, sm + (t % 3) * WSLOT, bh, bl, std::integral_constant<int, C1>{});
+    // keep the reload of f below its last use, so the ring slot stays in the same registers (an
+    // overlap would make the register allocator rotate the ring with copies that wait for the loads)
+    __builtin_amdgcn_sched_barrier(0);
+    load_f(t + 2, f);
+    kstep(acc0, sm + (t & 1) * WSLOT, bh, bl, std::integral_constant<int, C1>{}, no_hook);
   };
-  for (int t = 0; t < S0; t += 3) {
-    step0(t, fr[0]);
-    step0(t + 1, fr[1]);
-    step0(t + 2, fr[2]);
+  // prologue: W(0) -> LDS, W(1) -> registers, F(0), F(1); then the L0 steps as a do-while (S0 even),
+  // so the 2-deep input ring has a single entry path and stays in place across iterations
+  wload(0);
+  wstore(0);
+  if (T > 1) wload(1);
+  if (S0 > 0) {
+    float fa[2][8], fb[2][8];
+    load_f(0, fa);
+    load_f(1, fb);
+    int t = 0;
+    do {
+      step0(t, fa);
+      step0(t + 1, fb);
+      t += 2;
+    } while (t < S0);
   }
 
   using I1 = std::integral_constant<int, S1>;
   using I2 = std::integral_constant<int, S2>;
   using I3 = std::integral_constant<int, S3>;
-  // accumulators of a layer -> the next layer's B operands (bias + GELU + split, in registers)
-  auto to_operands = [&](auto& acc, half8 (*oh)[2], half8 (*ol)[2], auto nch_c, int boff, bool gelu, int wexp) {
-    constexpr int NCH = decltype(nch_c)::value;
+  // K-chunk c of a layer's accumulators -> the next layer's B operands (bias + GELU + split, in
+  // registers; 2^-wexp is exact, so the fma equals ldexp + add), one value pair at a time: pair pi =
+  // (j = pi >> 2, q = (pi >> 1) & 1, e = 2 (pi & 1)); the split of column block j follows its 4th pair
+  auto chunk_pair = [&](auto& acc, int c, int pi, float (&v)[2][8], half8 (&oh)[2], half8 (&ol)[2], int boff,
+                        float unscale) {
+    const int j = pi >> 2, q = (pi >> 1) & 1, e = 2 * (pi & 1);
+    const float* bq = sbias + boff + 32 * c + 16 * q + 4 * G + e;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float v[8];
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = boff + 32 * c + 16 * q + 4 * G + e;
-            float x = ldexpf(acc[2 * c + q][j][e], -wexp) + sbias[r];
-            v[4 * q + e] = gelu ? gelu_erf(x) : x;
-          }
-        split8(v, oh[c][j], ol[c][j], bad);
-      }
+    for (int k = 0; k < 2; ++k) v[j][4 * q + e + k] = gelu_erf(__builtin_fmaf(acc[2 * c + q][j][e + k], unscale, bq[k]));
+    if ((pi & 3) == 3) split8(v[j], oh[j], ol[j], bad);
   };
 
-  // one layer fed from registers: NCH K-chunks, COUT rows, steps t0 .. t0 + NCH - 1
-  auto layer_regs = [&](auto& acc, half8 (*bh)[2], half8 (*bl)[2], auto nch_c, auto cout_c, int t0) {
-    constexpr int NCH = decltype(nch_c)::value, COUT = decltype(cout_c)::value;
+  // one layer fed from the previous layer's accumulators: NCH K-chunks, COUT rows, steps t0 .. t0 +
+  // NCH - 1.  Chunk c + 1's operands are made during step c, spread over its MFMA blocks (VALU work
+  // independent of those MFMAs); chunk 0's before the first step.
+  auto layer_regs = [&](auto& acc, auto& prev, auto nch_c, auto cout_c, int t0, int boff, int wexp) {
+    constexpr int NCH = decltype(nch_c)::value, COUT = decltype(cout_c)::value, NBK = COUT / 16;
+    constexpr int PER = NBK >= 8 ? NBK / 8 : 1, PPB = NBK >= 8 ? 1 : 8 / NBK;  // blocks per pair, pairs per block
+    const float unscale = ldexpf(1.0f, -wexp);
 #pragma unroll
     for (int i = 0; i < COUT / 16; ++i)
       for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    half8 nh[2], nl[2];
+    float v[2][8];
+#pragma unroll
+    for (int pi = 0; pi < 8; ++pi) chunk_pair(prev, 0, pi, v, nh, nl, boff, unscale);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int t = t0 + c;
       step_begin(t);
-      const half8 b_h[2] = {bh[c][0], bh[c][1]}, b_l[2] = {bl[c][0], bl[c][1]};
-      kstep(acc, sm + (t % 3) * WSLOT, b_h, b_l, cout_c);
+      const half8 b_h[2] = {nh[0], nh[1]}, b_l[2] = {nl[0], nl[1]};
+      kstep(acc, sm + (t & 1) * WSLOT, b_h, b_l, cout_c, [&](int i) {
+        if (c + 1 < NCH && i % PER == 0)
+#pragma unroll
+          for (int k = 0; k < PPB; ++k) chunk_pair(prev, c + 1, (i / PER) * PPB + k, v, nh, nl, boff, unscale);
+      });
     }
   };
   // the output of the last layer: bias (+ residual), fp32 NCHW store
   auto store = [&](auto& acc, auto cout_c, int boff, int wexp) {
     constexpr int COUT = decltype(cout_c)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    range_report(P.rflag, bad);
+    range_report(P.rflag, bad != 0);
+#ifdef MLIC_CHAIN_TRACE
+    if (tr_wg >= 0 && lane == 0) {
+      CH_TR(T < CH_TR_STEPS ? T : CH_TR_STEPS - 1, 0);
+      for (int i = 0; i < CH_TR_STEPS * 3; ++i)
+        g_chain_trace[((int64_t)tr_wg * 4 + wv) * CH_TR_STEPS * 3 + i] = (&str[wv][0][0])[i];
+    }
+#endif
+    const float unscale = ldexpf(1.0f, -wexp);
 #pragma unroll
     for (int i = 0; i < COUT / 16; ++i)
 #pragma unroll
@@ -278,31 +309,25 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = 16 * i + 4 * G + e;
-          float v = ldexpf(acc[i][j][e], -wexp) + sbias[boff + co];
+          float v = __builtin_fmaf(acc[i][j][e], unscale, sbias[boff + co]);
           if (P.res) v += P.res[(int64_t)b * P.res_bs + (int64_t)co * HW + px];
           P.out[(int64_t)b * P.out_bs + (int64_t)co * HW + px] = v;
         }
       }
   };
 
-  half8 b1h[C1 / 32][2], b1l[C1 / 32][2];
-  to_operands(acc0, b1h, b1l, I1{}, 0, (P.gelu_mask & 1) != 0, P.wexp[0]);
   floatx4 acc1[C2 / 16][2];
-  layer_regs(acc1, b1h, b1l, I1{}, std::integral_constant<int, C2>{}, S0);
+  layer_regs(acc1, acc0, I1{}, std::integral_constant<int, C2>{}, S0, 0, P.wexp[0]);
   if constexpr (NL == 2) {
     store(acc1, std::integral_constant<int, C2>{}, C1, P.wexp[1]);
   } else {
-    half8 b2h[C2 / 32 > 0 ? C2 / 32 : 1][2], b2l[C2 / 32 > 0 ? C2 / 32 : 1][2];
-    to_operands(acc1, b2h, b2l, I2{}, C1, (P.gelu_mask & 2) != 0, P.wexp[1]);
     floatx4 acc2[C3 / 16][2];
-    layer_regs(acc2, b2h, b2l, I2{}, std::integral_constant<int, C3>{}, S0 + S1);
+    layer_regs(acc2, acc1, I2{}, std::integral_constant<int, C3>{}, S0 + S1, C1, P.wexp[1]);
     if constexpr (NL == 3) {
       store(acc2, std::integral_constant<int, C3>{}, C1 + C2, P.wexp[2]);
     } else {
-      half8 b3h[C3 / 32][2], b3l[C3 / 32][2];
-      to_operands(acc2, b3h, b3l, I3{}, C1 + C2, (P.gelu_mask & 4) != 0, P.wexp[2]);
       floatx4 acc3[C4 / 16][2];
-      layer_regs(acc3, b3h, b3l, I3{}, std::integral_constant<int, C4>{}, S0 + S1 + S2);
+      layer_regs(acc3, acc2, I3{}, std::integral_constant<int, C4>{}, S0 + S1 + S2, C1 + C2, P.wexp[2]);
       store(acc3, std::integral_constant<int, C4>{}, C1 + C2 + C3, P.wexp[3]);
     }
   }
@@ -345,8 +370,8 @@ bool chain_supported(int nl, const int* cout) {
 
 void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st) {
   MLIC_CHECK(chain_supported(nl, cout), "chain: unsupported layer widths");
-  MLIC_CHECK(P.cin0 % 32 == 0 && (P.cin0 > 0 || P.aux) && P.HW % 4 == 0 && P.HW >= 4,
-             "chain: Cin multiple of 32 (or 0 with aux), HW of 4");
+  MLIC_CHECK(P.cin0 % 64 == 0 && (P.cin0 > 0 || P.aux) && P.HW % 4 == 0 && P.HW >= 4,
+             "chain: Cin multiple of 64 (or 0 with aux), HW of 4");
   dim3 grid((P.HW + CH_BN - 1) / CH_BN, P.B);
   if (nl == 4 && cout[3] == 64)
     hipLaunchKernelGGL((chain_kernel<320, 256, 128, 64>), grid, dim3(CH_T), 0, st, P);

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(CONV_THREADS) void conv_mfma_kernel(ConvParams P) {
         if (co >= P.Cout) continue;
         float v = acc[i][j][r];
         if (P.bias) v += P.bias[co];
-        if (epi & EPI_GELU) v = gelu_erf(v);
+        if (epi & EPI_GELU) v = gelu_epi(v);
         if (epi & (EPI_GDN | EPI_IGDN)) {
           const float x = P.aux[(int64_t)b * P.aux_bs + (int64_t)co * HWo + p];
           v = (epi & EPI_GDN) ? x * (1.0f / sqrtf(v)) : x * sqrtf(v);

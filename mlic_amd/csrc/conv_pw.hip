@@ -226,7 +226,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
           // fp16 range guard on the accumulator (an input beyond fp16 splits to inf/NaN and poisons it;
           // checked before GDN, whose rsqrt(inf) = 0 would hide it); cheaper here than in the ring
           bad |= !(fabsf(v) <= 3.4e38f);
-          if (gelu) v = gelu_erf(v);
+          if (gelu) v = gelu_epi(v);
           if (gdn) v = gdn_apply(xa[r], v, igdn);
           v += xr[r];
           if (c * 32 + 32 <= P.Cout || co < P.Cout)

@@ -179,14 +179,14 @@ void gauss_likelihood(const float* y, const float* s, const float* m, int64_t n,
 void scale_indexes(const float* s, int64_t n, const float* table, int ntable, int32_t* idx, hipStream_t st);
 
 // fused 1x1 chain (chain.hip): layer widths cout[0..nl-1] in {320,256,128,64|128} (EntropyParameters)
-// or {128,64} (LocalContext MLP); weights pre-packed by chain_pack per layer, concatenated
+// or {128,64} (LocalContext MLP), GELU between layers; weights pre-packed by chain_pack per layer,
+// concatenated
 struct ChainParams {
   Seg seg[MAXSEG];
   int nseg, cin0;  // layer-0 input: channel concat, cin0 % 32 == 0
   int HW, B;       // pixels per image (HW % 4 == 0)
   const float* bias[4];
   int wexp[4];       // each layer's split weights are w * 2^wexp (split_weights)
-  int gelu_mask;   // bit l: GELU after layer l (l < nl - 1)
   const _Float16* wimg;
   float* out;      // [B][cout[nl-1]][HW] (batch stride out_bs)
   int64_t out_bs;

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], win[ky][q * S + kx], acc);
       float v = acc + bias;
-      if (P.gelu) v = gelu_erf(v);
+      if (P.gelu) v = gelu_epi(v);
       o[q] = v;
     }
     const int ox = ox0 + xs;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], win[(r + ky) % 3][q + kx], acc);
       float v = acc + bias;
-      if (P.gelu) v = gelu_erf(v);
+      if (P.gelu) v = gelu_epi(v);
       o[q] = v;
     }
     const int oy = oy0 + RPT * rg + r;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void dw3x3_s2_vec_kernel(DwParams P) {
   }
   if (P.gelu) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = gelu_erf(o[q]);
+    for (int q = 0; q < 4; ++q) o[q] = gelu_epi(o[q]);
   }
   const int oy = oy0 + ry, ox = ox0 + 4 * cg;
   if (oy < P.Ho && ox < P.Wo)

@@ -292,9 +292,9 @@ void Model::add_chains(hipStream_t st) {
       else if (w.Cin != c.cout[l - 1]) ok = false;
       total += chain_layer_halves(w.Cout, w.Cin);
     }
-    if (ok && chain_supported(c.nl, c.cout) && c.cin0 % 32 == 0) {
+    if (ok && chain_supported(c.nl, c.cout) && c.cin0 % 64 == 0) {  // even K-step count (chain.hip)
       cws.push_back(c);
-      if (c.nl == 4 && c.cin0 >= hyp && (c.cin0 - hyp) % 32 == 0) {  // the hoisted variant: context columns
+      if (c.nl == 4 && c.cin0 >= hyp && (c.cin0 - hyp) % 64 == 0) {  // the hoisted variant: context columns
         ChainW h = c;
         h.cin0 = c.cin0 - hyp;
         h.name = c.name + "#ctx";
@@ -633,7 +633,6 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
     P.bias[l] = c.bias[l];
     P.wexp[l] = c.wexp[l];
   }
-  P.gelu_mask = (1 << (c.nl - 1)) - 1;
   P.wimg = c.wimg;
   P.rflag = rflag_;
   P.out = out.p;

@@ -3,6 +3,7 @@ the C-ABI entry mlic_conv_run.  Shapes: the layer types of MLIC++ that each fami
 (g_a/g_s point convs and GDN/IGDN, subpel 3x3 convs with PixelShuffle, the N -> 12 output conv,
 the 3 -> N input convs, latent-resolution context GEMMs), plus ragged pixel counts."""
 import ctypes as C
+import math
 
 import pytest
 import torch
@@ -194,6 +195,35 @@ def test_depthwise(shape):
     if gelu:
         ref = F.gelu(ref)
     check(y, ref.float(), rtol=1e-6)
+
+
+def test_gelu_accuracy():
+    """The conv / depthwise epilogues' device GELU (common.h gelu_epi: torch's 0.5 x (1 + erf(x /
+    sqrt 2)) on the library erff) on a dense grid over [-12, 12]: its error vs the exact GELU (float64)
+    stays within 6 ulp of max(|x|, 2^-10), as torch's own fp32 GELU does (5.1).  (The chain kernel's
+    branch-free gelu_erf is pinned through the chain-vs-oracle parity tests.)  Driven through the
+    depthwise kernel with the centre tap 1 and zero bias, so y = gelu(x) exactly."""
+    from mlic_amd import _lib
+    dev = torch.device("cuda")
+    n = 1 << 20
+    xs = torch.linspace(-12.0, 12.0, n, dtype=torch.float32)
+    H, W = 1024, 1024
+    x = xs.reshape(1, 1, H, W).to(dev)
+    w = torch.zeros(1, 1, 3, 3, device=dev)
+    w[0, 0, 1, 1] = 1.0
+    b = torch.zeros(1, device=dev)
+    y = torch.full_like(x, float("nan"))
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("mlic_dw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()),
+              C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()), 1, 1, H, W, 1, 1)
+    torch.cuda.synchronize()
+    xd = xs.double()
+    exact = 0.5 * xd * torch.special.erfc(-xd / math.sqrt(2.0))
+    scale = torch.clamp(xs.abs(), min=2.0 ** -10)
+    ulp = (torch.nextafter(scale, torch.tensor(float("inf"))) - scale).double()
+    dev_ulps = ((y.cpu().reshape(-1).double() - exact).abs() / ulp).max().item()
+    torch_ulps = ((F.gelu(xs).double() - exact).abs() / ulp).max().item()
+    assert dev_ulps <= 6.0, (dev_ulps, torch_ulps)
 
 
 @pytest.mark.parametrize("ch,H,W,B", [(32, 24, 40, 2), (64, 13, 21, 1), (32, 68, 120, 1)])
