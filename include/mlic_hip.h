@@ -103,6 +103,10 @@ int mlic_profile_category_name(int cat, char* buf, size_t cap);
  * Synchronous on `stream`. */
 int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,
                   int Cout, int H, int W, int K, int stride, int epi, const float* aux, const float* res);
+/* the kernel family the model runs a conv layer of this shape with (precision 2; no GPU needed:
+ * host logic only) -> *impl.  Depends on the layer and one image's grid, never on B: the decoder must
+ * reproduce the encoder's entropy parameters bit for bit whatever batch either side uses. */
+int mlic_conv_choice(int B, int Cin, int Cout, int H, int W, int K, int stride, int epi, int* impl);
 /* depthwise 3x3 (pad 1, stride 1|2, optional GELU); w [C][9]; synchronous on `stream` */
 int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W,
                 int stride, int gelu);

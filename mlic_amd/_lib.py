@@ -51,6 +51,7 @@ def _sig(lib):
         "mlic_host_stats": [p, P(C.c_double), P(C.c_double), P(C.c_double), i],
         "mlic_profile_category_name": [i, p, sz],
         "mlic_conv_run": [p, i, p, p, p, p, i, i, i, i, i, i, i, i, p, p],
+        "mlic_conv_choice": [i, i, i, i, i, i, i, i, P(i)],
         "mlic_dw_run": [p, p, p, p, p, i, i, i, i, i, i],
         "mlic_local_attn_run": [p, i, p, p, p, p, i, i, i, i, f],
         "mlic_local_attn_packed_run": [p, p, p, p, p, i, i, i, f],

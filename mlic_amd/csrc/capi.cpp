@@ -320,6 +320,28 @@ int mlic_profile_category_name(int cat, char* buf, size_t cap) {
   });
 }
 
+int mlic_conv_choice(int B, int Cin, int Cout, int H, int W, int K, int stride, int epi, int* impl) {
+  return guard([&] {
+    MLIC_CHECK(impl && B > 0 && Cin > 0 && Cout > 0 && H > 0 && W > 0 && (K == 1 || K == 3 || K == 5) && stride > 0,
+               "conv_choice: bad arguments");
+    const int pad = K / 2;
+    ConvParams P{};
+    P.nseg = 1;
+    P.seg[0] = {nullptr, Cin, (int64_t)Cin * H * W};
+    P.Cin = Cin; P.H = H; P.W = W; P.Cout = Cout; P.K = K; P.stride = stride; P.pad = pad;
+    P.Ho = (H + 2 * pad - K) / stride + 1;
+    P.Wo = (W + 2 * pad - K) / stride + 1;
+    P.B = B;
+    P.epi = epi;
+    const int cin_pad = (Cin + 31) / 32 * 32;
+    // weight pointers only signal presence (the model holds split and x4 images for these layers)
+    static const _Float16 tag = 0;
+    const bool x4 = Cout >= 64;
+    const ConvWeights cw{nullptr, &tag, &tag, cin_pad, x4 ? &tag : nullptr, 0};
+    *impl = conv_select(P, cw, 2);
+  });
+}
+
 int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,
                   int Cout, int H, int W, int K, int stride, int epi, const float* aux, const float* res) {
   return guard([&] {

@@ -15,36 +15,43 @@ static bool x4_on() {
   return on;
 }
 
-// kernel sizes x4 takes (digits of $MLIC_X4_K, default "3"): the A/B switch for 1x1 / 5x5 layers
+// kernel sizes x4 takes (digits of $MLIC_X4_K, default "13"): the A/B switch for 1x1 / 5x5 layers
 static bool x4_k_on(int K) {
   static const int mask = [] {
     const char* e = std::getenv("MLIC_X4_K");
     int m = 0;
-    for (const char* c = e ? e : "3"; *c; ++c)
+    for (const char* c = e ? e : "13"; *c; ++c)
       if (*c >= '0' && *c <= '9') m |= 1 << (*c - '0');
     return m;
   }();
   return (mask >> K) & 1;
 }
 
+// The choice depends on the layer's shape and ONE image's grid, never on the batch: kernel families
+// round differently, and the decoder must rebuild the encoder's entropy parameters bit for bit
+// whatever batch either side runs (a stream coded in a batch of 8 decodes alone).  The grid-fill
+// thresholds are per image, sized for the bench's batches (8 per lane).
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (conv_smallcin_ok(P)) return CONV_SMALLCIN;  // exact fp32 VALU, all precisions
   if (conv_narrow_ok(P)) return CONV_NARROW;      // exact fp32 VALU, all precisions
   if (precision == 0 || !w.wh) return CONV_F32;
   if (precision == 1) return CONV_X3;
-  // resident weights pay once the grid fills the chip: >= 32 K pixels (1024 waves of 32-pixel tiles)
-  if ((int64_t)P.Ho * P.Wo * P.B >= 32768 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
-  // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs) once the grid fills the chip
-  if (w.wx4 && x4_on() && x4_k_on(P.K) && P.Cout >= (P.K == 3 ? 192 : 64) && conv_x4_ok(P, w.cin_pad)) {
+  // resident weights pay once the grid fills the chip: >= 4 K pixels per image
+  if ((int64_t)P.Ho * P.Wo >= 4096 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
+  // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs), and the big 1x1 GEMMs (the
+  // hoisted EntropyParameters hyper columns, h_s's last layer: Cin x Cout >= 2^18; smaller 1x1s
+  // measured even or slower than x3v2), once the grid fills the chip
+  const bool x4_shape = P.K == 1 ? (int64_t)P.Cin * P.Cout >= (1 << 18) : P.Cout >= (P.K == 3 ? 192 : 64);
+  if (w.wx4 && x4_on() && x4_k_on(P.K) && x4_shape && conv_x4_ok(P, w.cin_pad)) {
     const int bm = x4_bm(P.Cout);
     const int64_t rows = P.K == 1 ? ((int64_t)P.H * P.W + 31) / 32 : P.H;
     const int64_t cols = P.K == 1 ? 1 : (P.W + 31) / 32;
-    if ((int64_t)((P.Cout + bm - 1) / bm) * cols * ((rows + 7) / 8) * P.B >= 256) return CONV_X4;
+    if ((int64_t)((P.Cout + bm - 1) / bm) * cols * ((rows + 7) / 8) >= 32) return CONV_X4;
   }
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay
   if (P.K == 5 && conv_halo_ok(P, w.cin_pad) &&
-      (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 3) / 4) * P.B >= 64)
+      (int64_t)((P.Cout + 127) / 128) * ((P.Wo + 31) / 32) * ((P.Ho + 3) / 4) >= 8)
     return CONV_HALO;
   return CONV_X3V2;
 }

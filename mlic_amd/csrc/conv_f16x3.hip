@@ -537,7 +537,7 @@ int conv_x3v2_variant(const ConvParams& P) {
   const int64_t HWo = (int64_t)P.Ho * P.Wo;
   if (P.Cout <= 64) return 0;
   const int ct = (P.Cout + 255) / 256;
-  if (v2_wide() && P.Cout >= 192 && 4 * P.Cout >= 3 * 256 * ct && HWo * P.B >= 8192) return 3;
+  if (v2_wide() && P.Cout >= 192 && 4 * P.Cout >= 3 * 256 * ct && HWo >= 1024) return 3;  // per image (conv_select)
   if (P.Cout <= 192 && HWo >= 128 * 512) return 1;
   return 2;
 }
@@ -563,7 +563,7 @@ void conv_x3v2_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
   // Cout = 256k + r with r <= 128 (e.g. the entropy-parameters 640 -> 320 layer): the 256-row tiles
   // take 256k rows and a narrow tile the remainder, instead of 128-row tiles for everything
   const int r0 = 256 * (P.Cout / 256), rem = P.Cout - r0;
-  if (v == 2 && v2_wide() && r0 > 0 && rem > 0 && rem <= 128 && HWo * P.B >= 8192 && (r0 & 3) == 0) {
+  if (v == 2 && v2_wide() && r0 > 0 && rem > 0 && rem <= 128 && HWo >= 1024 && (r0 & 3) == 0) {
     const int64_t wofs = (int64_t)r0 * P.K * P.K * cin_pad;
     launch_v2<256, 256, 4, 2>(cout_slice(P, 0, r0), wh, wl, cin_pad, st);
     const ConvParams Q = cout_slice(P, r0, rem);

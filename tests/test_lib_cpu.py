@@ -1,5 +1,6 @@
 """CPU-side checks of libmlic_hip.so: it loads, exports the whole C ABI, and its host entropy
 coder / CDF quantizer match the restated compressai behaviour and the reference fixtures."""
+import ctypes as C
 import os
 import re
 
@@ -30,6 +31,26 @@ def test_null_handle_is_an_error_not_a_crash():
         _lib.call("mlic_host_stats", None, *[C.byref(v) for v in hs], 1)
     with pytest.raises(_lib.MlicError, match="null mlic_model handle"):
         _lib.call("mlic_set_lanes", None, 2)
+
+
+def test_conv_choice_is_batch_independent():
+    """The kernel family of every conv shape the models run (and a sweep around them) is the same for
+    any batch size: families round differently, and a stream coded in a batch must decode alone."""
+    shapes = []
+    for H, W in ((68, 120), (32, 48), (136, 240), (272, 480), (544, 960), (17, 30), (8, 12), (64, 64)):
+        for Cin, Cout, K in ((192, 192, 1), (128, 128, 1), (96, 96, 1), (160, 160, 1), (640, 6400, 1),
+                             (480, 640, 1), (496, 224, 1), (224, 128, 1), (128, 32, 1), (32, 96, 1),
+                             (192, 768, 3), (192, 192, 3), (320, 320, 5), (256, 64, 5), (3, 192, 1),
+                             (192, 12, 3), (320, 640, 3)):
+            for stride in ((1, 2) if K != 5 else (1,)):
+                shapes.append((Cin, Cout, H, W, K, stride))
+    impl = C.c_int()
+    for Cin, Cout, H, W, K, stride in shapes:
+        got = set()
+        for B in (1, 2, 3, 8, 16, 64):
+            _lib.call("mlic_conv_choice", B, Cin, Cout, H, W, K, stride, 0, C.byref(impl))
+            got.add(impl.value)
+        assert len(got) == 1, (Cin, Cout, H, W, K, stride, got)
 
 
 def test_gaussian_tables_match_reference_update(golden):
