@@ -47,7 +47,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
 # the split-fp16 kernels issue 3 fp16 MFMAs (2.5 PF dense) per fp32 product => 2500/3 TF of
 # fp32-equivalent work; the VALU kernels run exact fp32 FMAs (157.3 TF with packed FMA)
 def kernel_peak(name: str):
-    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv_halo", "conv_x4", "chain_")):
+    if name.startswith(("conv_f16x3", "conv_x3v2", "pw_resident", "conv_halo", "conv_x4", "chain_", "dwpw_")):
         return 2500.0 / 3, "3 x fp16 MFMA per fp32 product (split-fp16)"
     if name.startswith("local_attn"):
         return 2500.0 / 3, "3 x fp16 MFMA per fp32 product (split-fp16)"

@@ -110,6 +110,10 @@ int mlic_conv_choice(int B, int Cin, int Cout, int H, int W, int K, int stride, 
 /* depthwise 3x3 (pad 1, stride 1|2, optional GELU); w [C][9]; synchronous on `stream` */
 int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias, float* y, int B, int C, int H, int W,
                 int stride, int gelu);
+/* fused depthwise 3x3 (stride 1, pad 1; dww [C][9], dwb [C]) + pointwise 1x1 (w [Cout][C]) with
+ * epi in {0, GELU} | RES (res: [B][Cout][H][W]); C, Cout in {128, 192}; synchronous on `stream` */
+int mlic_dwpw_run(void* stream, const float* x, const float* dww, const float* dwb, const float* w, const float* bias,
+                  float* y, int B, int C, int Cout, int H, int W, int epi, const float* res);
 /* impl 0..2 as mlic_conv_run, 3 = the model's choice */
 int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
                     double* ms_per, double* tflops);

@@ -53,6 +53,7 @@ def _sig(lib):
         "mlic_conv_run": [p, i, p, p, p, p, i, i, i, i, i, i, i, i, p, p],
         "mlic_conv_choice": [i, i, i, i, i, i, i, i, P(i)],
         "mlic_dw_run": [p, p, p, p, p, i, i, i, i, i, i],
+        "mlic_dwpw_run": [p, p, p, p, p, p, p, i, i, i, i, i, i, p],
         "mlic_local_attn_run": [p, i, p, p, p, p, i, i, i, i, f],
         "mlic_local_attn_packed_run": [p, p, p, p, p, i, i, i, f],
         "mlic_image_sq_err_u8": [p, p, p, i, i64, p],

@@ -410,6 +410,33 @@ int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias,
   });
 }
 
+int mlic_dwpw_run(void* stream, const float* x, const float* dww, const float* dwb, const float* w, const float* bias,
+                  float* y, int B, int C, int Cout, int H, int W, int epi, const float* res) {
+  return guard([&] {
+    hipStream_t st = (hipStream_t)stream;
+    const int cin_pad = (C + 31) / 32 * 32;
+    const int64_t nh = (int64_t)Cout * cin_pad;
+    _Float16 *wh = nullptr, *wl = nullptr;
+    HIP_OK(hipMallocAsync((void**)&wh, nh * 2, st));
+    HIP_OK(hipMallocAsync((void**)&wl, nh * 2, st));
+    const int wexp = split_weights(w, wh, wl, Cout, C, 1, cin_pad, true, st);
+    ConvParams P{};
+    P.nseg = 1;
+    P.seg[0] = {x, C, (int64_t)C * H * W};
+    P.Cin = C; P.H = H; P.W = W; P.Cout = Cout; P.Ho = H; P.Wo = W; P.K = 1; P.stride = 1; P.pad = 0;
+    P.wexp = wexp; P.bias = bias; P.out = y; P.B = B; P.epi = epi;
+    P.out_cs = (int64_t)H * W;
+    P.out_bs = (int64_t)Cout * H * W;
+    MLIC_CHECK(!(epi & EPI_RES) || res, "residual epilogue needs res");
+    P.res = res; P.res_bs = P.out_bs;
+    MLIC_CHECK(dwpw_ok(P, cin_pad), "dwpw: unsupported shape");
+    dwpw_forward(P, wh, wl, cin_pad, dww, dwb, st);
+    HIP_OK(hipFreeAsync(wh, st));
+    HIP_OK(hipFreeAsync(wl, st));
+    HIP_OK(hipStreamSynchronize(st));
+  });
+}
+
 int mlic_local_attn_run(void* stream, int impl, const float* qkv, const float* rel_table, const int32_t* rel_index,
                         float* out, int C, int H, int W, int B, float scale) {
   return guard([&] {

@@ -111,7 +111,7 @@ const char* prof_cat_name(int cat) {
       "conv3x3_narrow_kernel",       "conv1x1_smallcin_kernel",   "conv_halo_kernel",
       "dw3x3_kernel",
       "local_attn_kernel",           "linear_attention",          "elementwise",
-      "conv_x4_kernel",              "chain_kernel"};
+      "conv_x4_kernel",              "chain_kernel",              "dwpw_kernel"};
   return (cat >= 0 && cat < PCAT_COUNT) ? names[cat] : "";
 }
 

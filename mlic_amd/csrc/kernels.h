@@ -32,6 +32,12 @@ void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* 
 bool conv_smallcin_ok(const ConvParams& P);
 void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 
+// fused depthwise 3x3 (stride 1, pad 1) + pointwise 1x1 (conv_dwpw.hip): P describes the pointwise
+// conv with the DEPTHWISE input as its input; dww [Cin][9], dwb [Cin]
+bool dwpw_ok(const ConvParams& P, int cin_pad);
+void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                  const float* dwb, hipStream_t st);
+
 // LDS-DMA split-fp16 conv (conv_x4.hip): activations packed per call into a zero-bordered split
 // layout (x4_pack_act, workspace of x4_act_halves halves), weights packed once (x4_pack_weights)
 int x4_bm(int Cout);
@@ -77,7 +83,8 @@ enum ProfCat : int {
   PCAT_ELEM = 19,
   PCAT_CONV_X4 = 20,
   PCAT_CHAIN = 21,
-  PCAT_COUNT = 22
+  PCAT_DWPW = 22,
+  PCAT_COUNT = 23
 };
 int conv_prof_cat(int impl, const ConvParams& P);
 const char* prof_cat_name(int cat);

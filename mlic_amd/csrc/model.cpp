@@ -392,6 +392,19 @@ bool Model::hoist_on() const {
   return on && chain_on() && hoist_.Cout > 0;
 }
 
+// $MLIC_DWPW=1: the fused depthwise+pointwise kernel (conv_dwpw.hip) for the stride-1 dwsep convs.
+// Off by default: measured slower than depthwise + resident pointwise on MI355X (g_a stage 1,
+// 8 x 192 x 544 x 960: 3.5 ms fused vs 1.29 + 1.77 ms; its per-k-step barrier keeps the whole
+// workgroup's store-issue-bound epilogue and VMEM-issue-bound staging from overlapping the MFMAs,
+// DESIGN.md).  Kept as the bit-exact reference point for the next design.
+bool Model::dwpw_on() const {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_DWPW");
+    return e && std::atoi(e) == 1;
+  }();
+  return on && precision_ == PREC_F16X3_V2;
+}
+
 // $MLIC_CHAIN=0: the per-layer path for EntropyParameters / LocalContext MLP (A/B switch)
 bool Model::chain_on() const {
   static const bool on = [] {
@@ -664,6 +677,17 @@ View Model::conv3x3(const std::vector<View>& ins, const std::string& p, int stri
   const DwW& d = dww(p + ".depth_conv");
   const ConvW& w = cw(p + ".point_conv");
   View out = out_opt ? *out_opt : alloc(w.Cout, Ho, Wo);
+  if (stride == 1 && dwpw_on() && w.wh && ins.size() == 1) {
+    // fused: the pointwise conv reads the depthwise input; the depthwise output stays on chip
+    ConvParams P = conv_params(ins, w, 1, 0, out, epi, nullptr, res);
+    if (dwpw_ok(P, w.cin_pad)) {
+      const double pix = (double)P.B * H * W;
+      const double flops = 2.0 * pix * P.Cin * (9 + w.Cout);
+      const double bytes = 4.0 * (pix * (P.Cin + w.Cout * (res ? 2 : 1)) + (double)w.Cout * P.Cin + 10.0 * P.Cin);
+      timed(PCAT_DWPW, flops, bytes, [&] { dwpw_forward(P, w.wh, w.wl, w.cin_pad, d.w, d.b, L().st); }, w.name);
+      return out;
+    }
+  }
   const size_t m = L().arena.mark();
   View t = alloc(d.C, Ho, Wo);
   dw(ins, d, stride, t, false);

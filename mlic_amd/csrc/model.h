@@ -186,6 +186,7 @@ class Model {
   void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
                  const View* aux = nullptr, int H = 0, int W = 0);
   bool chain_on() const;
+  bool dwpw_on() const;
   std::map<std::string, DwW> dws_;
   std::map<std::string, const float*> raw_;
   std::vector<void*> owned_;

@@ -197,6 +197,47 @@ def test_depthwise(shape):
     check(y, ref.float(), rtol=1e-6)
 
 
+@pytest.mark.parametrize("B,Cn,H,W,epi", [
+    (2, 192, 40, 100, 1),    # GELU; 100 columns = 3 segments of 30 + a ragged one
+    (1, 192, 17, 61, 0),     # odd sizes, last row block partial
+    (2, 192, 68, 120, 1 | 64),  # latent grid, GELU + residual
+    (1, 128, 24, 30, 0),     # Cin 128, one exact segment
+])
+def test_dwpw_fused(B, Cn, H, W, epi):
+    """Fused depthwise 3x3 + pointwise 1x1 (conv_dwpw.hip) == depthwise kernel then the resident-weight
+    pointwise kernel, bit for bit (same depthwise order, same MFMA k order), and within the split-fp16
+    tolerance of a float64 torch reference (DepthWiseConv, modules/layers/conv.py:22-32)."""
+    from mlic_amd import _lib
+    EPI_RES = 64
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    x = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
+    dw = ((torch.rand(Cn, 1, 3, 3, generator=g) - 0.5) * 0.6).to(dev)
+    db = (torch.rand(Cn, generator=g) - 0.5).to(dev)
+    w = ((torch.rand(Cn, Cn, 1, 1, generator=g) - 0.5) * 0.2).to(dev)
+    b = (torch.rand(Cn, generator=g) - 0.5).to(dev)
+    res = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
+    st = torch.cuda.current_stream().cuda_stream
+    y = torch.full((B, Cn, H, W), float("nan"), device=dev)
+    _lib.call("mlic_dwpw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
+              C.c_void_p(db.data_ptr()), C.c_void_p(w.data_ptr()), C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()),
+              B, Cn, Cn, H, W, epi, C.c_void_p(res.data_ptr()))
+    t = torch.full((B, Cn, H, W), float("nan"), device=dev)
+    _lib.call("mlic_dw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
+              C.c_void_p(db.data_ptr()), C.c_void_p(t.data_ptr()), B, Cn, H, W, 1, 0)
+    y2 = torch.full((B, Cn, H, W), float("nan"), device=dev)
+    _lib.call("mlic_conv_run", C.c_void_p(st), 3, C.c_void_p(t.data_ptr()), C.c_void_p(w.data_ptr()),
+              C.c_void_p(b.data_ptr()), C.c_void_p(y2.data_ptr()), B, Cn, Cn, H, W, 1, 1, epi, None,
+              C.c_void_p(res.data_ptr()))
+    assert torch.equal(y, y2)
+    ref = F.conv2d(F.conv2d(x.double(), dw.double(), db.double(), padding=1, groups=Cn), w.double(), b.double())
+    if epi & 1:
+        ref = F.gelu(ref)
+    if epi & EPI_RES:
+        ref = ref + res.double()
+    check(y, ref.float(), rtol=1e-6)
+
+
 def test_gelu_accuracy():
     """The conv / depthwise epilogues' device GELU (common.h gelu_epi: torch's 0.5 x (1 + erf(x /
     sqrt 2)) on the library erff) on a dense grid over [-12, 12]: its error vs the exact GELU (float64)
