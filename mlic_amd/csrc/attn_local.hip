@@ -64,10 +64,21 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_mfma_kernel(LocalAttnPa
   const int ntx = (W + LT_W - 1) / LT_W;
   const int x0 = (blockIdx.x % ntx) * LT_W, y0 = (blockIdx.x / ntx) * LT_H;
   const float* src = P.qkv + (int64_t)b * P.qkv_bs;
-  for (int i = threadIdx.x; i < 3 * C * NCELL; i += LA_THREADS) {
-    const int ch = i / NCELL, cell = i - ch * NCELL;
-    const int gy = y0 - 2 + cell / LW, gx = x0 - 2 + cell % LW;
-    sm[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? src[(int64_t)ch * HW + gy * W + gx] : 0.0f;
+  {  // all of this thread's loads in flight together, then the stores (see local_attn_packed_kernel)
+    constexpr int NSTG = 3 * C * NCELL, NQ = (NSTG + LA_THREADS - 1) / LA_THREADS;
+    float stg[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = threadIdx.x + q * LA_THREADS;
+      const int ch = i / NCELL, cell = i - ch * NCELL;
+      const int gy = y0 - 2 + cell / LW, gx = x0 - 2 + cell % LW;
+      stg[q] = (i < NSTG && gy >= 0 && gy < H && gx >= 0 && gx < W) ? src[(int64_t)ch * HW + gy * W + gx] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = threadIdx.x + q * LA_THREADS;
+      if (i < NSTG) sm[i] = stg[q];
+    }
   }
   float* ostage = sm + 3 * C * NCELL;  // [HD * 25][OPITCH] (STAGE only)
   __syncthreads();
@@ -82,13 +93,16 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_mfma_kernel(LocalAttnPa
 
   // relative-position bias for (query i = l32, key j of register r), both heads: item-invariant
   float bias[2][16];
+  int ridx[16];  // the index loads in flight together, then the table loads
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-      bias[hh][r] = (lvalid && j < 25) ? P.rel_table[P.rel_index[l32 * 25 + j] * 2 + hh] : 0.0f;
+    ridx[r] = (lvalid && j < 25) ? P.rel_index[l32 * 25 + j] : -1;
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) bias[hh][r] = ridx[r] >= 0 ? P.rel_table[ridx[r] * 2 + hh] : 0.0f;
 
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
@@ -223,14 +237,27 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
   const int ntx = (W + LP_TW - 1) / LP_TW;
   const int x0 = (blockIdx.x % ntx) * LP_TW, y0 = blockIdx.x / ntx;
   const float* src = P.qkv + (int64_t)b * P.qkv_bs;
-  for (int i = threadIdx.x; i < 3 * 32 * LP_NCP; i += LA_THREADS) {
+  // all of this thread's staging loads first (independent, in flight together), then the stores:
+  // a load -> convert -> store loop serialises one full memory latency per element
+  constexpr int NSTG = 3 * 32 * LP_NCP, NQ = (NSTG + LA_THREADS - 1) / LA_THREADS;
+  float stg[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = threadIdx.x + q * LA_THREADS;
     const int ch = i / LP_NCP, cell = i - ch * LP_NCP;
-    float v = 0.0f;
-    if (cell < LP_NCELL) {
+    stg[q] = 0.0f;
+    if (i < NSTG && cell < LP_NCELL) {
       const int gy = y0 - 2 + cell / LP_LW, gx = x0 - 2 + cell % LP_LW;
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = src[(int64_t)ch * HW + gy * W + gx];
-      if (ch < 32) v *= P.scale;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) stg[q] = src[(int64_t)ch * HW + gy * W + gx];
     }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = threadIdx.x + q * LA_THREADS;
+    if (i >= NSTG) break;
+    const int ch = i / LP_NCP, cell = i - ch * LP_NCP;
+    float v = stg[q];
+    if (ch < 32) v *= P.scale;
     const _Float16 hv = (_Float16)v, lv = (_Float16)(v - (float)hv);
     const int which = ch >> 5, c = ch & 31, d = c >> 1, hh = c & 1;  // channel = d * heads + head
     if (which < 2) {
@@ -253,13 +280,18 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
   // interior mask bits for pixel parity 0 / 1: register r allowed iff query and key cell are anchors
   uint32_t kbits[2] = {0u, 0u}, jbits = 0u;
   bool qok[2];
+  int ridx[16];  // the 16 index loads in flight together, then the 32 table loads
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
+    ridx[r] = (lvalid && j < 25) ? P.rel_index[l32 * 25 + j] : -1;
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
     const int jy = j / 5, jx = j - 5 * (j / 5);
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-      bias[hh][r] = (lvalid && j < 25) ? P.rel_table[P.rel_index[l32 * 25 + j] * 2 + hh] : 0.0f;
+    for (int hh = 0; hh < 2; ++hh) bias[hh][r] = ridx[r] >= 0 ? P.rel_table[ridx[r] * 2 + hh] : 0.0f;
     if (j < 25) {
       jbits |= 1u << r;
       kbits[(jy + jx + 1) & 1] |= 1u << r;  // (par + jy + jx) odd

@@ -41,10 +41,22 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(DwParams P) {
   int sg = 0, c0 = 0;
   while (sg + 1 < P.nseg && c >= c0 + P.seg[sg].C) { c0 += P.seg[sg].C; ++sg; }
   const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
-  for (int i = threadIdx.x; i < TWI * THI; i += 256) {
-    const int yy = i / TWI, xx = i - yy * TWI;
-    const int gy = iy0 + yy, gx = ix0 + xx;
-    tile[yy * PITCH + xx] = (gy >= 0 && gy < P.H && gx >= 0 && gx < P.W) ? src[(int64_t)gy * P.W + gx] : 0.0f;
+  {  // the patch loads in flight together, then the stores (a load -> store loop serialises them)
+    constexpr int NQ = (TWI * THI + 255) / 256;
+    float stg[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int yy = i / TWI, xx = i - yy * TWI;
+      const int gy = iy0 + yy, gx = ix0 + xx;
+      stg[q] = (i < TWI * THI && gy >= 0 && gy < P.H && gx >= 0 && gx < P.W) ? src[(int64_t)gy * P.W + gx] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int yy = i / TWI, xx = i - yy * TWI;
+      if (i < TWI * THI) tile[yy * PITCH + xx] = stg[q];
+    }
   }
   __syncthreads();
   float w[9];
@@ -105,12 +117,22 @@ __global__ __launch_bounds__(256) void dw3x3_s1_vec_kernel(DwParams P) {
   const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
   const int W4 = P.W >> 2;
   const float4* src4 = reinterpret_cast<const float4*>(src);
-  for (int i = threadIdx.x; i < DWF_PR * DWF_PQ; i += 256) {
-    const int r = i / DWF_PQ, q = i - r * DWF_PQ;
-    const int gy = oy0 - 1 + r, gq = (ox0 >> 2) - 1 + q;  // float4 column
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gy >= 0 && gy < P.H && gq >= 0 && gq < W4) v = src4[(int64_t)gy * W4 + gq];
-    tile[i] = v;
+  {  // the patch loads in flight together, then the stores
+    constexpr int NQ = (DWF_PR * DWF_PQ + 255) / 256;
+    float4 stg[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int r = i / DWF_PQ, q = i - r * DWF_PQ;
+      const int gy = oy0 - 1 + r, gq = (ox0 >> 2) - 1 + q;  // float4 column
+      stg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < DWF_PR * DWF_PQ && gy >= 0 && gy < P.H && gq >= 0 && gq < W4) stg[k] = src4[(int64_t)gy * W4 + gq];
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < DWF_PR * DWF_PQ) tile[i] = stg[k];
+    }
   }
   __syncthreads();
   float w[9];
@@ -168,12 +190,22 @@ __global__ __launch_bounds__(256) void dw3x3_s2_vec_kernel(DwParams P) {
   const float* src = P.seg[sg].p + (int64_t)b * P.seg[sg].bs + (int64_t)(c - c0) * P.H * P.W;
   const int W4 = P.W >> 2;
   const float4* src4 = reinterpret_cast<const float4*>(src);
-  for (int i = threadIdx.x; i < DW2_PR * DW2_PQ; i += 256) {
-    const int r = i / DW2_PQ, q = i - r * DW2_PQ;
-    const int gy = 2 * oy0 - 1 + r, gq = (2 * ox0 >> 2) - 1 + q;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gy >= 0 && gy < P.H && gq >= 0 && gq < W4) v = src4[(int64_t)gy * W4 + gq];
-    tile[i] = v;
+  {  // the patch loads in flight together, then the stores
+    constexpr int NQ = (DW2_PR * DW2_PQ + 255) / 256;
+    float4 stg[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int r = i / DW2_PQ, q = i - r * DW2_PQ;
+      const int gy = 2 * oy0 - 1 + r, gq = (2 * ox0 >> 2) - 1 + q;
+      stg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < DW2_PR * DW2_PQ && gy >= 0 && gy < P.H && gq >= 0 && gq < W4) stg[k] = src4[(int64_t)gy * W4 + gq];
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < DW2_PR * DW2_PQ) tile[i] = stg[k];
+    }
   }
   __syncthreads();
   float w[9];
