@@ -310,6 +310,11 @@ def main():
         c, d, enc_s, dec_s = last[gi]
         net = nets[(model, rate)]
         mses = mse_u8(xs[gi], d["x_hat"])
+        if len(groups) > 1:
+            # the device-side likelihood bits belong to a net's last compress(): groups sharing one
+            # net (vbr-mixed's 4K + 1080p) re-run this group's compress, untimed, to read them
+            kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
+            c = net.compress(xs[gi], **kw)
         for i, j in enumerate(js):
             nbytes = len(c["strings"][0][i]) + len(c["strings"][1][i])
             yb, zb = net.likelihood_bits(i)
