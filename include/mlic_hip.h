@@ -114,8 +114,9 @@ int mlic_dw_run(void* stream, const float* x, const float* w, const float* bias,
  * epi in {0, GELU} | RES (res: [B][Cout][H][W]); C, Cout in {128, 192}; synchronous on `stream` */
 int mlic_dwpw_run(void* stream, const float* x, const float* dww, const float* dwb, const float* w, const float* bias,
                   float* y, int B, int C, int Cout, int H, int W, int epi, const float* res);
-/* impl 0..2 as mlic_conv_run, 3 = the model's choice */
-int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
+/* impl as mlic_conv_run (CONV_* ids), < 0 = the model's choice; epi = Epi flags (RES in place,
+   GDN/IGDN with the input as operand) */
+int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int epi, int iters,
                     double* ms_per, double* tflops);
 int mlic_local_attn_mask(void* stream, float* out, int H, int W); /* [H*W, 25, 25] of {0, -100} */
 /* LocalContext window attention: qkv [B][3C][H*W] -> out [B][25C][H*W]; impl 0 = VALU, 1 = MFMA */

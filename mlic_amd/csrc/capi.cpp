@@ -226,7 +226,7 @@ int mlic_profile_layers(mlic_model* m, char* buf, size_t cap, size_t* written) {
 
 // conv micro-benchmark: random operands of one layer shape, `iters` launches timed with events.
 // impl: 0 = conv_mfma (fp32), 1 = conv_f16x3.  Returns ms per launch and TFLOP/s (algorithmic).
-int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int shuffle, int iters,
+int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int stride, int epi, int iters,
                     double* ms_per, double* tflops) {
   return guard([&] {
     const int pad = K / 2;
@@ -260,14 +260,25 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     P.wpk = wp; P.bias = bias; P.out = y; P.B = B;
     P.out_bs = (int64_t)Cout * Ho * Wo;
     P.out_cs = (int64_t)Ho * Wo;
-    P.epi = shuffle ? EPI_SHUFFLE : 0;
+    P.epi = epi;
+    MLIC_CHECK(!(epi & (EPI_GDN | EPI_IGDN | EPI_SHUFFLE)) || !(epi & EPI_RES), "bench: unsupported epilogue");
+    if (epi & (EPI_GDN | EPI_IGDN)) {  // the conv input doubles as the GDN operand (Cin == Cout)
+      MLIC_CHECK(Cin == Cout && stride == 1, "bench: GDN needs Cin == Cout");
+      P.aux = x;
+      P.aux_bs = (int64_t)Cin * H * W;
+    }
+    if (epi & EPI_RES) {  // in place, as the LRP head's residual into y_hat
+      P.res = y;
+      P.res_bs = P.out_bs;
+    }
     _Float16* wx = nullptr;
     if (conv_x4_ok(P, cin_pad)) {
       HIP_OK(hipMalloc((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2));
       x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, nullptr);
     }
     const ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
-    const int which = impl == 3 ? conv_select(P, cw, 2) : impl;  // 3 = what the model runs (precision 2)
+    const int which = impl < 0 ? conv_select(P, cw, 2) : impl;  // < 0: what the model runs (precision 2)
+    if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
     if (which == CONV_X4) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
     void* ws = nullptr;
     const int64_t wsb = conv_ws_bytes(which, P, cw);

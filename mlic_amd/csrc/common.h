@@ -118,7 +118,8 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // the conv / depthwise epilogues' GELU: torch's own formula 0.5 x (1 + erf(x / sqrt 2)) on the
 // library erff.  Its branches keep those epilogues' fully unrolled element loops small (the
 // branch-free gelu_erf, evaluated for every element there, pushes them past the unroller's budget or
-// up in registers); gelu_erf serves the chain kernel, where it is interleaved with MFMAs
+// up in registers); gelu_erf serves the chain kernel, where it is interleaved with MFMAs, and the
+// pw_resident / dwpw epilogues, whose element loops are short
 __device__ __forceinline__ float gelu_epi(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }

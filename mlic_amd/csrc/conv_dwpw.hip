@@ -265,7 +265,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
         float v = ldexpf(acc[c][r], -wexp);
         v += sb[c * 32 + (r & 3) + 8 * (r >> 2)];
         bad |= !(fabsf(v) <= 3.4e38f);
-        if (GELU) v = gelu_epi(v);
+        if (GELU) v = gelu_erf(v);
         v += xr[r];
         if (c * 32 + 32 <= P.Cout || co < P.Cout)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);

@@ -51,7 +51,8 @@ __device__ __forceinline__ void opaque(uint32_t& v) { asm volatile("" : "+s"(v))
 template <int CIN>
 constexpr int pw_apitch() { return CIN + 8; }  // halves; +16 B per row spreads rows over the banks
 
-// MODE: 0 = bias only, 1 = GELU, 2 = GDN (x * rsqrt), 3 = IGDN (x * sqrt); residual add at run time
+// MODE: 0 = bias only, 1 = GELU, 2 = GDN (x * rsqrt), 3 = IGDN (x * sqrt), 4 = 0.5 tanh + the
+// checkerboard mask of P.epi (the LRP head); residual add (RES) last
 template <int CIN, int CT, int MODE, bool RES>
 __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, const _Float16* __restrict__ wh,
                                                                   const _Float16* __restrict__ wl, int cin_pad) {
@@ -65,17 +66,32 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
 
   const int tid = threadIdx.x;
   constexpr int QPR = CIN / 8;  // 16-byte chunks per weight row
-  for (int id = tid; id < ROWS * QPR; id += PW_THREADS) {
+  // every weight load issued before the first LDS store: one memory latency for the whole prologue
+  // (a load -> store loop pays one per iteration, which is most of a latent-resolution launch)
+  constexpr int NIT = (ROWS * QPR + PW_THREADS - 1) / PW_THREADS;
+  uint4 wst[2 * NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int id = tid + it * PW_THREADS;
     const int row = id / QPR, q = id - row * QPR;
-    uint4 h = make_uint4(0, 0, 0, 0), l = make_uint4(0, 0, 0, 0);
-    if (row < P.Cout) {
-      h = *reinterpret_cast<const uint4*>(wh + (int64_t)row * cin_pad + 8 * q);
-      l = *reinterpret_cast<const uint4*>(wl + (int64_t)row * cin_pad + 8 * q);
+    wst[2 * it] = wst[2 * it + 1] = make_uint4(0, 0, 0, 0);
+    if (id < ROWS * QPR && row < P.Cout) {
+      wst[2 * it] = *reinterpret_cast<const uint4*>(wh + (int64_t)row * cin_pad + 8 * q);
+      wst[2 * it + 1] = *reinterpret_cast<const uint4*>(wl + (int64_t)row * cin_pad + 8 * q);
     }
-    *reinterpret_cast<uint4*>(sm + row * APITCH + 8 * q) = h;
-    *reinterpret_cast<uint4*>(sm + A_SZ + row * APITCH + 8 * q) = l;
   }
-  for (int r = tid; r < ROWS; r += PW_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
+  const float bias_v = (tid < ROWS && P.bias && tid < P.Cout) ? P.bias[tid] : 0.0f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int id = tid + it * PW_THREADS;
+    const int row = id / QPR, q = id - row * QPR;
+    if (id < ROWS * QPR) {
+      *reinterpret_cast<uint4*>(sm + row * APITCH + 8 * q) = wst[2 * it];
+      *reinterpret_cast<uint4*>(sm + A_SZ + row * APITCH + 8 * q) = wst[2 * it + 1];
+    }
+  }
+  static_assert(ROWS <= PW_THREADS, "one bias per thread");
+  if (tid < ROWS) sbias[tid] = bias_v;
   __syncthreads();
 
   const int lane = tid & 63;
@@ -88,7 +104,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
   int tile = blockIdx.x * PW_WAVES + wave;
   if (tile >= ntiles) return;  // no barrier follows
 
-  constexpr bool square = MODE >= 2;  // GDN/IGDN convolve x*x
+  constexpr bool square = MODE == 2 || MODE == 3;  // GDN/IGDN convolve x*x
   const float* xbase = P.seg[0].p;
   const int64_t xbs = P.seg[0].bs;
   const uint32_t hw4 = (uint32_t)(P.H * P.W) * 4u;  // input plane (stride 2: the full-resolution plane)
@@ -108,7 +124,10 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
 
   // load ring: D = KS/2 k-steps ahead.  Slot j % D holds k-step j of the current tile until it is
   // consumed, then receives k-step j + D (of this tile, or of the next one for j >= KS - D).
-  constexpr int D = KS / 2;
+#ifndef MLIC_PW_RING  // tuning knob: ring depth in k-steps, 0 = KS / 2, 1 = KS (a whole tile ahead), 2 = 3 KS / 4
+#define MLIC_PW_RING 0
+#endif
+  constexpr int D = MLIC_PW_RING == 1 ? KS : MLIC_PW_RING == 2 ? (3 * KS) / 4 : KS / 2;
   float ring[D][8];
   {
     const auto rs = rsrc_of(tile);
@@ -187,7 +206,13 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
     const uint32_t cs4 = (uint32_t)P.out_cs * 4u;
     const uint32_t vo_out = (uint32_t)p * 4u + (uint32_t)(4 * h) * cs4;
     const auto rs_out = make_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
-    constexpr bool gdn = MODE >= 2, igdn = MODE == 3, gelu = MODE == 1;
+    constexpr bool gdn = MODE == 2 || MODE == 3, igdn = MODE == 3, gelu = MODE == 1, tanh_mask = MODE == 4;
+    // checkerboard mask: keep v where this pixel's anchor-ness matches the flag (MODE 4 only)
+    bool keep = true;
+    if (tanh_mask && (P.epi & (EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR))) {
+      const int oh = p / P.Wo, ow = p - oh * P.Wo;
+      keep = is_anchor(oh, ow) == ((P.epi & EPI_MASK_ANCHOR) != 0);
+    }
     constexpr bool res = RES;
     const auto rs_aux = make_rsrc(gdn ? P.aux + (int64_t)b * P.aux_bs : P.out, gdn ? (uint32_t)P.Cout * ho4 : 0u);
     const uint32_t vo_aux = (uint32_t)p * 4u + (uint32_t)(4 * h) * ho4;
@@ -213,24 +238,46 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
           if (gdn) xa[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_aux, vo_aux, oa, 0));
           xr[r] = res ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, vo_out, oo, 0)) : 0.0f;
         }
-        oo = so_o;
+        // biases of this co-tile: rows 32c + 8g + 4h .. +3 as four 16-byte LDS reads
+        float4 bq[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bq[g] = *reinterpret_cast<const float4*>(sb + c * 32 + 8 * g);
+        float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int co = c * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (r > 0) {
-            oo += (((r & 3) == 0) ? 5u : 1u) * cs4;
-            opaque(oo);
-          }
-          float v = ldexpf(acc[c][r], -wexp);
-          v += sb[c * 32 + (r & 3) + 8 * (r >> 2)];
+          const float4 b4 = bq[r >> 2];
+          const float bv = (r & 3) == 0 ? b4.x : (r & 3) == 1 ? b4.y : (r & 3) == 2 ? b4.z : b4.w;
+          float x = ldexpf(acc[c][r], -wexp) + bv;
           // fp16 range guard on the accumulator (an input beyond fp16 splits to inf/NaN and poisons it;
           // checked before GDN, whose rsqrt(inf) = 0 would hide it); cheaper here than in the ring
-          bad |= !(fabsf(v) <= 3.4e38f);
-          if (gelu) v = gelu_epi(v);
-          if (gdn) v = gdn_apply(xa[r], v, igdn);
-          v += xr[r];
-          if (c * 32 + 32 <= P.Cout || co < P.Cout)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
+          bad |= !(fabsf(x) <= 3.4e38f);
+          if (gelu) x = gelu_erf(x);
+          if (gdn) x = gdn_apply(xa[r], x, igdn);
+          if (tanh_mask) x = keep ? 0.5f * tanhf(x) : 0.0f;
+          v[r] = x + xr[r];
+        }
+        // straight-line stores for a full co-tile (the uniform common case); per-row guards only on
+        // the ragged last one
+        oo = so_o;
+        if (c * 32 + 32 <= P.Cout) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (r > 0) {
+              oo += (((r & 3) == 0) ? 5u : 1u) * cs4;
+              opaque(oo);
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs_out, vo_out, oo, 0);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (r > 0) {
+              oo += (((r & 3) == 0) ? 5u : 1u) * cs4;
+              opaque(oo);
+            }
+            if (c * 32 + (r & 3) + 8 * (r >> 2) + 4 * h < P.Cout)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[r]), rs_out, vo_out, oo, 0);
+          }
         }
         so_o += 32 * cs4;
         so_a += 32 * ho4;
@@ -252,57 +299,76 @@ static int num_cus() {
   return n;
 }
 
+// epilogue mode of P (see the kernel's MODE), -1 when the kernel has none for it
+static int pw_mode(const ConvParams& P) {
+  const int e = P.epi & ~EPI_RES;
+  if (e == EPI_NONE) return 0;
+  if (e == EPI_GELU) return 1;
+  if (e == (EPI_GDN | EPI_SQUARE_IN)) return 2;
+  if (e == (EPI_IGDN | EPI_SQUARE_IN)) return 3;
+  if (e == EPI_TANH_HALF || e == (EPI_TANH_HALF | EPI_MASK_ANCHOR) || e == (EPI_TANH_HALF | EPI_MASK_NONANCHOR))
+    return 4;
+  return -1;
+}
+
+// instantiated (CIN, CT, MODE, RES) tuples.  PW_ALL: Cin = Cout = 32 CT, every epilogue (g_a / g_s
+// point convs, GDN / IGDN, at full and half resolution).  The single tuples are the latent-resolution
+// 1x1 convs of the context models and the LRP (MLICPP_L, slice_ch 32): there the generic tiles
+// hold one output tile per CU and spend the launch in load latency, while this kernel streams
+// 32-pixel columns from every wave of every CU.
+#define PW_ALL(X, CIN, CT) \
+  X(CIN, CT, 0, 0) X(CIN, CT, 0, 1) X(CIN, CT, 1, 0) X(CIN, CT, 1, 1) \
+  X(CIN, CT, 2, 0) X(CIN, CT, 2, 1) X(CIN, CT, 3, 0) X(CIN, CT, 3, 1)
+#define PW_COMBOS(X)                                                                              \
+  PW_ALL(X, 96, 3) PW_ALL(X, 128, 4) PW_ALL(X, 160, 5) PW_ALL(X, 192, 6)                          \
+  /* LRP: 224 -> 128 GELU; head 128 -> 32 (0.5 tanh, checkerboard mask, residual into y_hat) */   \
+  X(224, 4, 1, 0) X(128, 1, 4, 1)                                                                 \
+  /* channel context (dwsep): 32i -> 192 GELU, 192 -> 128 GELU */                                 \
+  X(32, 6, 1, 0) X(64, 6, 1, 0) X(96, 6, 1, 0) X(128, 6, 1, 0) X(160, 6, 1, 0) X(192, 4, 1, 0)   \
+  /* inter/intra q/k/v (dim -> dim), local qkv_proj 32 -> 96, proj 64 -> 64 */                   \
+  X(32, 1, 0, 0) X(64, 2, 0, 0) X(32, 3, 0, 0)                                                    \
+  /* global contexts: mlp.0 GELU (96 -> 128, 64 -> 128), mlp.4 + residual 128 -> 64, skip */      \
+  X(96, 4, 1, 0) X(64, 4, 1, 0) X(128, 2, 0, 1) X(96, 2, 0, 0)
+
 bool pw_resident_ok(const ConvParams& P, int cin_pad) {
   if (P.K != 1 || (P.stride != 1 && P.stride != 2) || P.pad != 0 || P.nseg != 1) return false;
-  if (P.epi & ~(EPI_GELU | EPI_GDN | EPI_IGDN | EPI_SQUARE_IN | EPI_RES)) return false;
-  if ((P.epi & EPI_GELU) && (P.epi & (EPI_GDN | EPI_IGDN))) return false;
-  if (((P.epi & (EPI_GDN | EPI_IGDN)) != 0) != ((P.epi & EPI_SQUARE_IN) != 0)) return false;
+  const int mode = pw_mode(P);
+  if (mode < 0) return false;
   if (P.Ho != (P.H - 1) / P.stride + 1 || P.Wo != (P.W - 1) / P.stride + 1) return false;
   if (P.seg[0].C != P.Cin || cin_pad != P.Cin) return false;
-  if (P.stride != 1 && (P.epi & (EPI_GDN | EPI_IGDN))) return false;  // GDN aux is the conv input
+  if (P.stride != 1 && (mode == 2 || mode == 3 || mode == 4)) return false;  // GDN aux is the conv input; mask grid
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
   const int ct = (P.Cout + 31) / 32;
-  switch (P.Cin) {
-    case 96: return ct == 3;
-    case 128: return ct == 4;
-    case 160: return ct == 5;
-    case 192: return ct == 6;
-    default: return false;
-  }
+  const int res = (P.epi & EPI_RES) ? 1 : 0;
+#define MLIC_PW_OK(CIN, CT, M, R) \
+  if (P.Cin == CIN && ct == CT && mode == M && res == R) return true;
+  PW_COMBOS(MLIC_PW_OK)
+#undef MLIC_PW_OK
+  return false;
 }
 
-template <int CIN, int CT>
+template <int CIN, int CT, int M, bool R>
 static void launch_pw(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   const int64_t ntiles = (int64_t)((P.Ho * P.Wo + 31) / 32) * P.B;
   const int64_t want = (ntiles + PW_WAVES - 1) / PW_WAVES;
   const dim3 grid((unsigned)std::min<int64_t>(want, (int64_t)num_cus()));
-  const int mode = (P.epi & EPI_GELU) ? 1 : (P.epi & EPI_GDN) ? 2 : (P.epi & EPI_IGDN) ? 3 : 0;
-  const bool res = (P.epi & EPI_RES) != 0;
-#define MLIC_PW(M, R) \
-  hipLaunchKernelGGL((pw_resident_kernel<CIN, CT, M, R>), grid, dim3(PW_THREADS), 0, st, P, wh, wl, cin_pad)
-  switch (mode * 2 + (res ? 1 : 0)) {
-    case 0: MLIC_PW(0, false); break;
-    case 1: MLIC_PW(0, true); break;
-    case 2: MLIC_PW(1, false); break;
-    case 3: MLIC_PW(1, true); break;
-    case 4: MLIC_PW(2, false); break;
-    case 5: MLIC_PW(2, true); break;
-    case 6: MLIC_PW(3, false); break;
-    default: MLIC_PW(3, true); break;
-  }
-#undef MLIC_PW
+  hipLaunchKernelGGL((pw_resident_kernel<CIN, CT, M, R>), grid, dim3(PW_THREADS), 0, st, P, wh, wl, cin_pad);
   HIP_OK(hipGetLastError());
 }
 
 void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
-  switch (P.Cin) {
-    case 96: launch_pw<96, 3>(P, wh, wl, cin_pad, st); break;
-    case 128: launch_pw<128, 4>(P, wh, wl, cin_pad, st); break;
-    case 160: launch_pw<160, 5>(P, wh, wl, cin_pad, st); break;
-    default: launch_pw<192, 6>(P, wh, wl, cin_pad, st); break;
+  const int mode = pw_mode(P);
+  const int ct = (P.Cout + 31) / 32;
+  const int res = (P.epi & EPI_RES) ? 1 : 0;
+#define MLIC_PW_RUN(CIN, CT, M, R)                                  \
+  if (P.Cin == CIN && ct == CT && mode == M && res == R) {          \
+    launch_pw<CIN, CT, M, R != 0>(P, wh, wl, cin_pad, st);          \
+    return;                                                         \
   }
+  PW_COMBOS(MLIC_PW_RUN)
+#undef MLIC_PW_RUN
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -530,14 +530,21 @@ void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed
   const double flops = 2.0 * outn * P.Cin * w.K * w.K;
   const double bytes = 4.0 * ((double)P.B * P.Cin * P.H * P.W + (double)w.Cout * P.Cin * w.K * w.K +
                               outn * (1 + (P.aux ? 1 : 0) + (P.res ? 1 : 0)));
+  // profile tag: layer name + shape (Cin>Cout kK sS, epilogue flags, input segments)
+  std::string tag;
+  if (L().prof) {
+    char sh[96];
+    std::snprintf(sh, sizeof sh, " [%d>%d k%d s%d e%x n%d]", P.Cin, P.Cout, P.K, P.stride, P.epi, P.nseg);
+    tag = w.name + sh;
+  }
   if (packed) {
-    timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_x4_forward(P, packed, w.wx4, w.cin_pad, L().st); }, w.name);
+    timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_x4_forward(P, packed, w.wx4, w.cin_pad, L().st); }, tag);
     return;
   }
   const int64_t wsb = conv_ws_bytes(impl, P, cw);
   const size_t m = L().arena.mark();
   void* ws = wsb > 0 ? static_cast<void*>(L().arena.alloc((wsb + 3) / 4)) : nullptr;
-  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st, ws); }, w.name);
+  timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_run(impl, P, cw, L().st, ws); }, tag);
   L().arena.release(m);  // stream-ordered: the next user of this memory runs after the conv
 }
 

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-GELU, GDN, IGDN, RES, SHUFFLE, SQUARE = 1, 2, 4, 64, 128, 256
+GELU, GDN, IGDN, TANH, MASK_A, MASK_N, RES, SHUFFLE, SQUARE = 1, 2, 4, 8, 16, 32, 64, 128, 256
 F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, X4, AUTO = 0, 1, 2, 3, 4, 5, 6, 7, -1
 
 
@@ -23,6 +23,13 @@ def reference(x, w, b, stride, epi, res):
         y = x * torch.rsqrt(y)
     if epi & IGDN:
         y = x * torch.sqrt(y)
+    if epi & TANH:
+        y = 0.5 * torch.tanh(y)
+    if epi & (MASK_A | MASK_N):  # checkerboard: anchor cells have (h + w) odd
+        hh = torch.arange(y.shape[-2], device=y.device).view(-1, 1)
+        ww = torch.arange(y.shape[-1], device=y.device).view(1, -1)
+        anchor = ((hh + ww) % 2) == 1
+        y = y * (anchor if epi & MASK_A else ~anchor).to(y.dtype)
     if epi & SHUFFLE:
         y = F.pixel_shuffle(y, 2)
     if epi & RES:
@@ -75,6 +82,18 @@ def test_pw_resident_epilogues(epi):
 def test_pw_resident_stride2():
     check(*run(PW, 2, 192, 192, 68, 96, 1, stride=2))
     check(*run(PW, 1, 128, 128, 37, 51, 1, stride=2, epi=GELU))  # odd sizes: ragged tiles
+
+
+# the latent-resolution 1x1 convs (MLICPP_L): LRP 224 -> 128 and its head 128 -> 32 (0.5 tanh,
+# checkerboard mask, residual), channel-context 32i -> 192 / 192 -> 128, context q/k/v, qkv_proj,
+# proj, mlp.0 / mlp.4 (+ residual) and skip
+@pytest.mark.parametrize("cin,cout,epi", [
+    (224, 128, GELU), (128, 32, TANH | MASK_A | RES), (128, 32, TANH | MASK_N | RES),
+    (32, 192, GELU), (64, 192, GELU), (96, 192, GELU), (128, 192, GELU), (160, 192, GELU), (192, 128, GELU),
+    (32, 32, 0), (64, 64, 0), (32, 96, 0), (96, 128, GELU), (64, 128, GELU), (128, 64, RES), (96, 64, 0)])
+def test_pw_resident_latent(cin, cout, epi):
+    check(*run(PW, 2, cin, cout, 68, 120, 1, epi=epi))
+    check(*run(PW, 1, cin, cout, 37, 53, 1, epi=epi, seed=1))  # ragged: tail tile, odd width for the mask
 
 
 def test_pw_resident_ragged_and_many_tiles():
