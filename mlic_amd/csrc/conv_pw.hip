@@ -124,10 +124,9 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
 
   // load ring: D = KS/2 k-steps ahead.  Slot j % D holds k-step j of the current tile until it is
   // consumed, then receives k-step j + D (of this tile, or of the next one for j >= KS - D).
-#ifndef MLIC_PW_RING  // tuning knob: ring depth in k-steps, 0 = KS / 2, 1 = KS (a whole tile ahead), 2 = 3 KS / 4
-#define MLIC_PW_RING 0
-#endif
-  constexpr int D = MLIC_PW_RING == 1 ? KS : MLIC_PW_RING == 2 ? (3 * KS) / 4 : KS / 2;
+  // (measured: a ring of 3/4 or all of KS, and non-temporal loads / stores, change nothing: the
+  // TA -> TCP path is the limit, busy ~80 % of the launch with the TCP's pending-miss stall ~85 %)
+  constexpr int D = KS / 2;
   float ring[D][8];
   {
     const auto rs = rsrc_of(tile);
@@ -182,6 +181,14 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
       }
       // keep the reload here: the scheduler would otherwise hoist the ring's loads above the MFMAs
       __builtin_amdgcn_sched_barrier(0);
+#ifndef MLIC_PW_ABL  // diagnostics: 1 = one MFMA per k-step, 2 = no output stores, 3 = both
+#define MLIC_PW_ABL 0
+#endif
+      if (MLIC_PW_ABL & 1) {
+        const half8 ah0 = *reinterpret_cast<const half8*>(Ah + 16 * j);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bh + bl, acc[0], 0, 0, 0);
+        continue;
+      }
       // co-tiles in pairs so consecutive MFMAs never chain on one accumulator
 #pragma unroll
       for (int c = 0; c < CT; c += 2) {
@@ -259,6 +266,9 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
         // straight-line stores for a full co-tile (the uniform common case); per-row guards only on
         // the ragged last one
         oo = so_o;
+        if ((MLIC_PW_ABL & 2) && P.Cout > 0) {  // uniform: keeps the stores in the code, skips them
+          asm volatile("" :: "v"(v[0]), "v"(v[5]), "v"(v[10]), "v"(v[15]));
+        } else
         if (c * 32 + 32 <= P.Cout) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
