@@ -122,13 +122,12 @@ void local_attn_valu(const LocalAttnParams& P, hipStream_t st);
 // (channel head*16 + d), the B operand of the fusion conv with its K permuted to cell*32 + channel
 void local_attn_packed(const LocalAttnParams& P, _Float16* out, int npos, hipStream_t st);
 
-void softmax_spatial(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int mask_mode,
-                     hipStream_t st);
-void softmax_channel(const float* x, int64_t x_bs, float* y, int64_t y_bs, int heads, int hd, int H, int W, int B,
-                     int mask_mode, hipStream_t st);
+// context.py:180-187 / 235-239 in three launches (no materialised softmax); kmask: anchor-only keys,
+// qmask: non-anchor-only queries; part: linear_attention_part_floats() floats
+int64_t linear_attention_part_floats(int heads, int hd, int B, int nsplit);
 void linear_attention(const float* K, int64_t k_bs, const float* V, int64_t v_bs, const float* Q, int64_t q_bs,
-                      float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int HW, int B,
-                      int nsplit, hipStream_t st);
+                      float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int H, int W, int B,
+                      int nsplit, int kmask, int qmask, hipStream_t st);
 void ckbd_mask(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int keep_anchor,
                hipStream_t st);
 

@@ -5,10 +5,9 @@
 //  ln_channels ...... nn.LayerNorm over channels of an NCHW map (context.py:73, 110)
 //  local_attn ....... LocalContext windowed 5x5 attention (context.py:75-107): q/k/v halo tile in
 //                     LDS, Swin relative-position bias, checkerboard mask computed from parity bits
-//  softmax_spatial .. F.softmax(keys, dim=L) (context.py:180, 235), optional anchor-only support
-//  softmax_channel .. F.softmax(queries, dim=head channels) (context.py:181, 236)
-//  ctx_partial/reduce K.V^T over L as a split reduction with a fixed-order combine
-//  attn_apply ....... ctx^T . Q (context.py:187, 239)
+//  ctx_partial/reduce softmax_L(K).V^T over L as a split reduction with a max-rescaled fixed-order
+//                     combine (F.softmax(keys, dim=L), context.py:180, 235, never materialised)
+//  attn_apply ....... ctx^T . softmax_c(Q) (context.py:181, 187, 236, 239)
 //  quant / likelihood / indexes / dequant: ste_round, GaussianConditional, build_indexes,
 //                     checkerboard phases (mlicpp.py:112-138, ckbd.py:123-220)
 //  eb_forward ....... EntropyBottleneck factorized likelihood + median rounding (compressai)
@@ -408,183 +407,207 @@ void local_attn_valu(const LocalAttnParams& P, hipStream_t st) {
 }
 
 // =============================================================================================
-// softmax over the spatial axis of each (b, channel) row; mask_mode 1 => only anchor positions
-// participate (others output 0): the intra-slice "keys" over the squeezed anchor half.
-__global__ __launch_bounds__(256) void softmax_spatial_kernel(const float* __restrict__ x, int64_t x_bs,
-                                                              float* __restrict__ y, int64_t y_bs, int H, int W,
-                                                              int mask_mode) {
-  __shared__ float red[256];
-  const int c = blockIdx.x, b = blockIdx.y;
-  const int HW = H * W;
-  const float* xr = x + (int64_t)b * x_bs + (int64_t)c * HW;
-  float* yr = y + (int64_t)b * y_bs + (int64_t)c * HW;
-  auto active = [&](int p) { return mask_mode == 0 || is_anchor(p / W, p % W); };
-  float mx = -3.0e38f;
-  for (int p = threadIdx.x; p < HW; p += 256)
-    if (active(p)) mx = fmaxf(mx, xr[p]);
-  red[threadIdx.x] = mx;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  mx = red[0];
-  __syncthreads();
-  float sum = 0.0f;
-  for (int p = threadIdx.x; p < HW; p += 256)
-    if (active(p)) sum += expf(xr[p] - mx);
-  red[threadIdx.x] = sum;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  const float inv = 1.0f / red[0];
-  for (int p = threadIdx.x; p < HW; p += 256) yr[p] = active(p) ? expf(xr[p] - mx) * inv : 0.0f;
-}
-
-void softmax_spatial(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int mask_mode,
-                     hipStream_t st) {
-  hipLaunchKernelGGL(softmax_spatial_kernel, dim3(C, B), dim3(256), 0, st, x, x_bs, y, y_bs, H, W, mask_mode);
-  HIP_OK(hipGetLastError());
-}
-
-// softmax over the hd channels of each head at each pixel; mask_mode 2 => output only at
-// non-anchor pixels (intra-slice queries), 0 elsewhere
-template <int HD>
-__global__ void softmax_channel_kernel(const float* __restrict__ x, int64_t x_bs, float* __restrict__ y,
-                                       int64_t y_bs, int heads, int H, int W, int mask_mode) {
-  constexpr int hd = HD;
-  const int HW = H * W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int h = blockIdx.y % heads, b = blockIdx.y / heads;
-  if (p >= HW) return;
-  const float* xp = x + (int64_t)b * x_bs + (int64_t)h * hd * HW + p;
-  float* yp = y + (int64_t)b * y_bs + (int64_t)h * hd * HW + p;
-  if (mask_mode == 2 && is_anchor(p / W, p % W)) {
-    for (int d = 0; d < hd; ++d) yp[(int64_t)d * HW] = 0.0f;
-    return;
-  }
-  float v[HD];
-  float mx = -3.0e38f;
-#pragma unroll
-  for (int d = 0; d < hd; ++d) { v[d] = xp[(int64_t)d * HW]; mx = fmaxf(mx, v[d]); }
-  float sum = 0.0f;
-#pragma unroll
-  for (int d = 0; d < hd; ++d) { v[d] = expf(v[d] - mx); sum += v[d]; }
-  const float inv = 1.0f / sum;
-#pragma unroll
-  for (int d = 0; d < hd; ++d) yp[(int64_t)d * HW] = v[d] * inv;
-}
-
-void softmax_channel(const float* x, int64_t x_bs, float* y, int64_t y_bs, int heads, int hd, int H, int W, int B,
-                     int mask_mode, hipStream_t st) {
-  const dim3 grid((H * W + 127) / 128, heads * B);
-  if (hd == 16) hipLaunchKernelGGL(softmax_channel_kernel<16>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, heads, H, W, mask_mode);
-  else if (hd == 32) hipLaunchKernelGGL(softmax_channel_kernel<32>, grid, dim3(128), 0, st, x, x_bs, y, y_bs, heads, H, W, mask_mode);
-  else MLIC_CHECK(false, "head dim must be 16 or 32");
-  HIP_OK(hipGetLastError());
-}
-
-// ctx[b][h][c][d] = sum_p K[b][h*hd+c][p] * V[b][h*hd+d][p], split over NSPLIT chunks of p,
-// partials combined in a fixed order by ctx_reduce (bitwise reproducible, no atomics)
+// Linear attention (context.py:180-187, 235-239): out = ctx^T . softmax_c(Q) with
+// ctx = softmax_L(K) . V^T, without materialising either softmax:
+//  * ctx_partial: per (image, head, split of L) the per-channel max m_s of the split's active keys,
+//    sum_p exp(k - m_s) v (a register-tiled K.V^T) and sum_p exp(k - m_s);
+//  * ctx_reduce: the splits combined in a fixed order with the max-rescaling exp(m_s - M), then the
+//    division by the total exp-sum (bitwise reproducible, no atomics);
+//  * attn_apply: the channel softmax of each pixel's query in registers, then ctx^T . q.
+// kmask = 1: only anchor positions are keys (the intra-slice squeezed anchor half); qmask = 1: only
+// non-anchor positions have queries (outputs 0 at anchors).
 constexpr int CTX_CHUNK = 64;
 
+// record per (image, head, split): [HD] key maxima m_s, [HD][HD] sum_p exp(k_c - m_s) v_d,
+// [HD] sum_p exp(k_c - m_s).  256 threads; the K.V^T tile of thread t is a TC x TC block
+// (TC = HD / 16) read from pixel-major LDS copies as float2 pairs.
+template <int HD>
 __global__ __launch_bounds__(256) void ctx_partial_kernel(const float* __restrict__ K, int64_t k_bs,
                                                           const float* __restrict__ V, int64_t v_bs,
-                                                          float* __restrict__ part, int heads, int hd, int HW,
-                                                          int nsplit) {
-  __shared__ float ks[32][CTX_CHUNK + 1];
-  __shared__ float vs[32][CTX_CHUNK + 1];
+                                                          float* __restrict__ part, int heads, int H, int W,
+                                                          int nsplit, int kmask) {
+  constexpr int KP = HD + 2;                  // row pitch (floats): float2-aligned, 2-way write conflicts
+  constexpr int NE = HD * CTX_CHUNK / 256;    // staged elements per thread per chunk: c = wave + 4 j, pixel = lane
+  constexpr int TC = HD / 16;
+  __shared__ __attribute__((aligned(16))) float kt[CTX_CHUNK][KP];
+  __shared__ __attribute__((aligned(16))) float vt[CTX_CHUNK][KP];
+  __shared__ float mxs[HD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int split = blockIdx.x, h = blockIdx.y % heads, b = blockIdx.y / heads;
+  const int HW = H * W;
   const int per = (HW + nsplit - 1) / nsplit;
   const int pbeg = split * per, pend = min(HW, pbeg + per);
-  const float* kb = K + (int64_t)b * k_bs + (int64_t)h * hd * HW;
-  const float* vb = V + (int64_t)b * v_bs + (int64_t)h * hd * HW;
-  const int nout = hd * hd;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* kb = K + (int64_t)b * k_bs + (int64_t)h * HD * HW;
+  const float* vb = V + (int64_t)b * v_bs + (int64_t)h * HD * HW;
+  auto active = [&](int p) { return kmask == 0 || is_anchor(p / W, p % W); };
+  // pass 1: the split's per-channel key maximum, one wave per channel
+  for (int c = wave; c < HD; c += 4) {
+    float m = -3.0e38f;
+    for (int p = pbeg + lane; p < pend; p += 64)
+      if (active(p)) m = fmaxf(m, kb[(int64_t)c * HW + p]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) mxs[c] = m;
+  }
+  __syncthreads();
+  float mloc[NE];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) mloc[j] = mxs[wave + 4 * j];
+  float ssum[NE];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) ssum[j] = 0.0f;
+  const int c0 = (tid >> 4) * TC, d0 = (tid & 15) * TC;
+  float acc[TC][TC];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int k = 0; k < TC; ++k) acc[i][k] = 0.0f;
   for (int p0 = pbeg; p0 < pend; p0 += CTX_CHUNK) {
-    for (int i = threadIdx.x; i < hd * CTX_CHUNK; i += 256) {
-      const int c = i / CTX_CHUNK, pp = i % CTX_CHUNK;
-      const int p = p0 + pp;
-      ks[c][pp] = p < pend ? kb[(int64_t)c * HW + p] : 0.0f;
-      vs[c][pp] = p < pend ? vb[(int64_t)c * HW + p] : 0.0f;
+    const int p = p0 + lane;
+    const bool in = p < pend, on = in && active(p);
+    float kv[NE], vv[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {  // loads first, one latency per chunk
+      const int64_t off = (int64_t)(wave + 4 * j) * HW + p;
+      kv[j] = on ? kb[off] : 0.0f;
+      vv[j] = in ? vb[off] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const float e = on ? expf(kv[j] - mloc[j]) : 0.0f;
+      ssum[j] += e;
+      kt[lane][wave + 4 * j] = e;
+      vt[lane][wave + 4 * j] = vv[j];
     }
     __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = threadIdx.x + r * 256;
-      if (o < nout) {
-        const int c = o / hd, d = o % hd;
-        float a = acc[r];
-        for (int pp = 0; pp < CTX_CHUNK; ++pp) a = fmaf(ks[c][pp], vs[d][pp], a);
-        acc[r] = a;
+#pragma unroll 8
+    for (int pp = 0; pp < CTX_CHUNK; ++pp) {
+      if constexpr (TC == 2) {
+        const float2 a = *reinterpret_cast<const float2*>(&kt[pp][c0]);
+        const float2 v = *reinterpret_cast<const float2*>(&vt[pp][d0]);
+        acc[0][0] = fmaf(a.x, v.x, acc[0][0]);
+        acc[0][1] = fmaf(a.x, v.y, acc[0][1]);
+        acc[1][0] = fmaf(a.y, v.x, acc[1][0]);
+        acc[1][1] = fmaf(a.y, v.y, acc[1][1]);
+      } else {
+        acc[0][0] = fmaf(kt[pp][c0], vt[pp][d0], acc[0][0]);
       }
     }
     __syncthreads();
   }
-  float* dst = part + (((int64_t)b * heads + h) * nsplit + split) * nout;
+  float* dst = part + (((int64_t)b * heads + h) * nsplit + split) * (HD * (HD + 2));
+  if (tid < HD) dst[tid] = mxs[tid];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int o = threadIdx.x + r * 256;
-    if (o < nout) dst[o] = acc[r];
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int k = 0; k < TC; ++k) dst[HD + (c0 + i) * HD + d0 + k] = acc[i][k];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {  // fixed butterfly; lane 0's value is the record
+    float t = ssum[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) dst[HD + HD * HD + wave + 4 * j] = t;
   }
 }
 
-__global__ void ctx_reduce_kernel(const float* __restrict__ part, float* __restrict__ ctx, int nout, int nsplit,
+__global__ void ctx_reduce_kernel(const float* __restrict__ part, float* __restrict__ ctx, int hd, int nsplit,
                                   int total) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over (b*heads) * nout
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over (b*heads) * hd * hd
   if (i >= total) return;
-  const int bh = i / nout, o = i % nout;
-  const float* src = part + (int64_t)bh * nsplit * nout + o;
-  float s = 0.0f;
-  for (int k = 0; k < nsplit; ++k) s += src[(int64_t)k * nout];
-  ctx[i] = s;
+  const int nout = hd * hd, rec = hd * (hd + 2);
+  const int bh = i / nout, o = i % nout, c = o / hd;
+  const float* src = part + (int64_t)bh * nsplit * rec;
+  float M = -3.0e38f;
+  for (int k = 0; k < nsplit; ++k) M = fmaxf(M, src[(int64_t)k * rec + c]);
+  float num = 0.0f, den = 0.0f;
+  for (int k = 0; k < nsplit; ++k) {
+    const float* r = src + (int64_t)k * rec;
+    const float w = expf(r[c] - M);
+    num = fmaf(w, r[hd + o], num);
+    den = fmaf(w, r[hd + nout + c], den);
+  }
+  ctx[i] = num / den;
 }
 
-// out[b][h*hd+d][p] = sum_c ctx[b][h][c][d] * Q[b][h*hd+c][p]
+// out[b][h*hd+d][p] = sum_c ctx[b][h][c][d] * softmax_c(Q[b][h*hd+c][p]); ctx rows read as float4
 template <int HD>
 __global__ __launch_bounds__(256) void attn_apply_kernel(const float* __restrict__ ctx, const float* __restrict__ Q,
                                                          int64_t q_bs, float* __restrict__ out, int64_t o_bs,
-                                                         int heads, int HW) {
+                                                         int heads, int H, int W, int qmask) {
   constexpr int hd = HD;
-  __shared__ float cs[32 * 32];
+  __shared__ __attribute__((aligned(16))) float cs[HD * HD];
+  const int HW = H * W;
   const int h = blockIdx.y % heads, b = blockIdx.y / heads;
   const float* cb = ctx + ((int64_t)b * heads + h) * hd * hd;
   for (int i = threadIdx.x; i < hd * hd; i += 256) cs[i] = cb[i];
   __syncthreads();
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= HW) return;
+  float* op = out + (int64_t)b * o_bs + (int64_t)h * hd * HW + p;
+  if (qmask && is_anchor(p / W, p % W)) {
+    for (int d = 0; d < hd; ++d) op[(int64_t)d * HW] = 0.0f;
+    return;
+  }
   const float* qp = Q + (int64_t)b * q_bs + (int64_t)h * hd * HW + p;
   float q[HD];
+  float mx = -3.0e38f;
 #pragma unroll
-  for (int c = 0; c < hd; ++c) q[c] = qp[(int64_t)c * HW];
-  float* op = out + (int64_t)b * o_bs + (int64_t)h * hd * HW + p;
-  for (int d = 0; d < hd; ++d) {
-    float a = 0.0f;
-#pragma unroll
-    for (int c = 0; c < hd; ++c) a = fmaf(cs[c * hd + d], q[c], a);
-    op[(int64_t)d * HW] = a;
+  for (int c = 0; c < hd; ++c) {
+    q[c] = qp[(int64_t)c * HW];
+    mx = fmaxf(mx, q[c]);
   }
+  float sum = 0.0f;
+#pragma unroll
+  for (int c = 0; c < hd; ++c) {
+    q[c] = expf(q[c] - mx);
+    sum += q[c];
+  }
+  const float inv = 1.0f / sum;
+#pragma unroll
+  for (int c = 0; c < hd; ++c) q[c] *= inv;
+  float a[HD];
+#pragma unroll
+  for (int d = 0; d < hd; ++d) a[d] = 0.0f;
+#pragma unroll
+  for (int c = 0; c < hd; ++c) {
+#pragma unroll
+    for (int d4 = 0; d4 < hd / 4; ++d4) {
+      const float4 w = *reinterpret_cast<const float4*>(&cs[c * hd + 4 * d4]);  // broadcast
+      a[4 * d4] = fmaf(w.x, q[c], a[4 * d4]);
+      a[4 * d4 + 1] = fmaf(w.y, q[c], a[4 * d4 + 1]);
+      a[4 * d4 + 2] = fmaf(w.z, q[c], a[4 * d4 + 2]);
+      a[4 * d4 + 3] = fmaf(w.w, q[c], a[4 * d4 + 3]);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < hd; ++d) op[(int64_t)d * HW] = a[d];
+}
+
+int64_t linear_attention_part_floats(int heads, int hd, int B, int nsplit) {
+  return (int64_t)B * heads * nsplit * (hd * (hd + 2));
 }
 
 void linear_attention(const float* K, int64_t k_bs, const float* V, int64_t v_bs, const float* Q, int64_t q_bs,
-                      float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int HW, int B,
-                      int nsplit, hipStream_t st) {
+                      float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int H, int W, int B,
+                      int nsplit, int kmask, int qmask, hipStream_t st) {
   MLIC_CHECK(hd == 16 || hd == 32, "head dim");
-  hipLaunchKernelGGL(ctx_partial_kernel, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads, hd,
-                     HW, nsplit);
+  const int HW = H * W;
+  if (hd == 16)
+    hipLaunchKernelGGL(ctx_partial_kernel<16>, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads,
+                       H, W, nsplit, kmask);
+  else
+    hipLaunchKernelGGL(ctx_partial_kernel<32>, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads,
+                       H, W, nsplit, kmask);
   HIP_OK(hipGetLastError());
   const int total = B * heads * hd * hd;
-  hipLaunchKernelGGL(ctx_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, ctx, hd * hd, nsplit,
-                     total);
+  hipLaunchKernelGGL(ctx_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, ctx, hd, nsplit, total);
   HIP_OK(hipGetLastError());
   if (hd == 16)
     hipLaunchKernelGGL(attn_apply_kernel<16>, dim3((HW + 255) / 256, heads * B), dim3(256), 0, st, ctx, Q, q_bs, out,
-                       o_bs, heads, HW);
+                       o_bs, heads, H, W, qmask);
   else
     hipLaunchKernelGGL(attn_apply_kernel<32>, dim3((HW + 255) / 256, heads * B), dim3(256), 0, st, ctx, Q, q_bs, out,
-                       o_bs, heads, HW);
+                       o_bs, heads, H, W, qmask);
   HIP_OK(hipGetLastError());
 }
 

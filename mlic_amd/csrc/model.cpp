@@ -940,16 +940,14 @@ View Model::inter_context(const View& x, int i) {
   View q = qkv_branch(x, p + ".queries");
   View k = qkv_branch(x, p + ".keys");
   View v = qkv_branch(x, p + ".values");
-  View ks = alloc(D, H, W);
-  View qs = alloc(D, H, W);
   View att = alloc(D, H, W);
   const int nsplit = ctx_splits(HW);
-  float* part = L().arena.alloc((int64_t)L().B * heads * nsplit * hd * hd);
+  float* part = L().arena.alloc(linear_attention_part_floats(heads, hd, L().B, nsplit));
   float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
-  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
-    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 0, L().st);
-    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 0, L().st);
-    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
+  // algorithmic bytes: k, v, q read once, the output written once
+  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 4.0, [&] {
+    linear_attention(k.p, k.bs, v.p, v.bs, q.p, q.bs, att.p, att.bs, part, ctx, heads, hd, H, W, L().B, nsplit, 0, 0,
+                     L().st);
   }, p + ".attn");
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
@@ -980,16 +978,13 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   View q = qkv_branch(x1n, p + ".queries");
   View k = qkv_branch(x1a, p + ".keys");
   View v = qkv_branch(x2, p + ".values");
-  View ks = alloc(D, H, W);
-  View qs = alloc(D, H, W);
   View att = alloc(D, H, W);
   const int nsplit = ctx_splits(HW);
-  float* part = L().arena.alloc((int64_t)L().B * heads * nsplit * hd * hd);
+  float* part = L().arena.alloc(linear_attention_part_floats(heads, hd, L().B, nsplit));
   float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
-  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 6.0, [&] {
-    softmax_spatial(k.p, k.bs, ks.p, ks.bs, D, H, W, L().B, 1, L().st);
-    softmax_channel(q.p, q.bs, qs.p, qs.bs, heads, hd, H, W, L().B, 2, L().st);
-    linear_attention(ks.p, ks.bs, v.p, v.bs, qs.p, qs.bs, att.p, att.bs, part, ctx, heads, hd, HW, L().B, nsplit, L().st);
+  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 4.0, [&] {
+    linear_attention(k.p, k.bs, v.p, v.bs, q.p, q.bs, att.p, att.bs, part, ctx, heads, hd, H, W, L().B, nsplit, 1, 2,
+                     L().st);
   }, p + ".attn");
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
