@@ -168,7 +168,7 @@ __device__ __forceinline__ void conv_store(const ConvParams& P, int b, int co, i
 // shuffle).  conv_store_shuf4: under PixelShuffle(2), channels co0 (= 4 oc + 2 dy) and co0 + 1 at
 // pixels p, p+1 fill x2 = 2 ow .. 2 ow + 3 of output row 2 oh + dy; v = (co0@p, co0+1@p, co0@p+1,
 // co0+1@p+1).  Callers check 16-byte alignment of every operand (conv_vec_ok) and full validity.
-__device__ __forceinline__ bool conv_vec_ok(const ConvParams& P) {
+__host__ __device__ __forceinline__ bool conv_vec_ok(const ConvParams& P) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(P.out) | reinterpret_cast<uintptr_t>(P.aux) |
                       reinterpret_cast<uintptr_t>(P.res);
   return (a & 15) == 0 && ((P.out_bs | P.out_cs | P.aux_bs | P.res_bs) & 3) == 0 && (P.Wo & 3) == 0;

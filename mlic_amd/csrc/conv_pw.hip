@@ -22,7 +22,8 @@
 //    ds_read_b128 straight into v_pk_fma_f32 operands) staged through LDS in 8-channel chunks.
 //
 // 3. conv1x1_smallcin_kernel — 1x1 convs with Cin <= 4 (g_a's first point conv and skip, 3 -> N):
-//    write-bound; one pixel per lane, Cout outputs from scalar weights.
+//    write-bound; one pixel per lane (four per lane with 16-byte stores where rows allow), Cout
+//    outputs from scalar weights.
 #include "common.h"
 #include "kernels.h"
 
@@ -570,12 +571,56 @@ __global__ __launch_bounds__(256) void conv1x1_smallcin_kernel(ConvParams P) {
   }
 }
 
+// the same with four consecutive output pixels of one row per lane and 16-byte stores (the layer is
+// write-bound: Cout = N outputs per input pixel); identical per-element arithmetic
+template <int CIN>
+__global__ __launch_bounds__(256) void conv1x1_smallcin_vec_kernel(ConvParams P) {
+  const int HWo = P.Ho * P.Wo;
+  const int p = 4 * (blockIdx.x * 256 + threadIdx.x);
+  const int b = blockIdx.y;
+  if (p >= HWo) return;
+  const int oh = p / P.Wo, ow = p - oh * P.Wo;
+  const int64_t HWi = (int64_t)P.H * P.W;
+  const int S = P.stride;
+  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs + (int64_t)(oh * S) * P.W + ow * S;
+  float xv[CIN][4];
+#pragma unroll
+  for (int c = 0; c < CIN; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xv[c][e] = x[c * HWi + e * S];
+      if (P.epi & EPI_SQUARE_IN) xv[c][e] *= xv[c][e];
+    }
+  const float* w = P.wpk;  // [1][Cin][Cout]
+  for (int co = 0; co < P.Cout; ++co) {
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) {
+      const float wc = w[c * P.Cout + co];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaf(xv[c][e], wc, v[e]);
+    }
+    conv_store4(P, b, co, p, make_float4(v[0], v[1], v[2], v[3]));
+  }
+}
+
 bool conv_smallcin_ok(const ConvParams& P) {
   return P.K == 1 && P.pad == 0 && P.nseg == 1 && P.Cin >= 1 && P.Cin <= 4;
 }
 
 void conv_smallcin_forward(const ConvParams& P, hipStream_t st) {
   MLIC_CHECK(conv_smallcin_ok(P), "conv_smallcin: unsupported shape");
+  if ((P.Wo & 3) == 0 && conv_vec_ok(P) && !(P.epi & EPI_SHUFFLE)) {
+    dim3 grid((P.Ho * P.Wo / 4 + 255) / 256, P.B);
+    switch (P.Cin) {
+      case 1: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<1>, grid, dim3(256), 0, st, P); break;
+      case 2: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<2>, grid, dim3(256), 0, st, P); break;
+      case 3: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<3>, grid, dim3(256), 0, st, P); break;
+      default: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<4>, grid, dim3(256), 0, st, P); break;
+    }
+    HIP_OK(hipGetLastError());
+    return;
+  }
   dim3 grid((P.Ho * P.Wo + 255) / 256, P.B);
   switch (P.Cin) {
     case 1: hipLaunchKernelGGL(conv1x1_smallcin_kernel<1>, grid, dim3(256), 0, st, P); break;

@@ -110,7 +110,9 @@ def test_narrow(epi):
 
 @pytest.mark.parametrize("stride", [1, 2])
 def test_smallcin(stride):
-    check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride))
+    check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride))               # 4-pixel vector path
+    check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride, epi=GELU | RES))
+    check(*run(SMALLCIN, 1, 3, 192, 37, 53, 1, stride=stride, epi=GELU))      # odd width: scalar path
 
 
 @pytest.mark.parametrize("impl", [F32, X3, X3V2])
