@@ -74,7 +74,8 @@ int conv_prof_cat(int impl, const ConvParams& P) {
 }
 
 int64_t conv_ws_bytes(int impl, const ConvParams& P, const ConvWeights& w) {
-  return impl == CONV_X4 ? 2 * x4_act_halves(P, w.cin_pad) : 0;
+  // x4: the packed activations, then (256-byte aligned) the split-K partial planes
+  return impl == CONV_X4 ? (2 * x4_act_halves(P, w.cin_pad) + 255) / 256 * 256 + x4_part_bytes(P, w.cin_pad) : 0;
 }
 
 void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t st, void* ws) {
@@ -94,8 +95,10 @@ void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t 
     case CONV_X4: {
       MLIC_CHECK(ws && w.wx4, "conv_x4: workspace and packed weights required");
       _Float16* act = static_cast<_Float16*>(ws);
+      const int64_t abytes = (2 * x4_act_halves(P, w.cin_pad) + 255) / 256 * 256;
+      float* part = x4_part_bytes(P, w.cin_pad) > 0 ? reinterpret_cast<float*>(static_cast<char*>(ws) + abytes) : nullptr;
       x4_pack_act(P, w.cin_pad, act, st);
-      conv_x4_forward(P, act, w.wx4, w.cin_pad, st);
+      conv_x4_forward(P, act, w.wx4, w.cin_pad, st, part);
       break;
     }
     default: throw Error("mlic: unknown conv implementation " + std::to_string(impl));

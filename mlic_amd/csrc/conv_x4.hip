@@ -62,7 +62,7 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 template <int K, int BM, bool RS>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
                                                       const _Float16* __restrict__ wx, int nchunk, int H, int W,
-                                                      int abl) {
+                                                      int abl, int nsplit) {
   constexpr int KK = K * K;
   constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WN = BN / WAVES_N;        // pixels per wave
@@ -90,8 +90,12 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   }
   const int ct = logical % nct, pt = logical / nct;
   const int oy0 = (pt / ntx) * TR, ox0 = (pt % ntx) * TC;
-  const int b = blockIdx.z;
+  // split-K (nsplit > 1): blockIdx.z = image + B * split; the block runs steps [s0, s1) and stores
+  // its raw partial sums into plane `split` of the partial buffer (P carries that layout, no epilogue)
+  const int b = blockIdx.z % P.B, split = blockIdx.z / P.B;
   const int nsteps = nchunk * KK;
+  const int s0 = split * nsteps / nsplit, s1 = (split + 1) * nsteps / nsplit;
+  if (nsplit > 1) P.out += (int64_t)split * P.B * P.out_bs;
 
   // per-lane DMA sources.  B: instruction i of this wave moves pixels n = (wave*NB + i)*8 + lane/8,
   // physical granule lane%8 <- logical granule (lane%8) ^ swz(n).  Pixels past the image edge read a
@@ -149,17 +153,17 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       for (int i = 0; i < NA; ++i)
         *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave * NA + i) * 1024 + lane * 16) = ra[i];
     };
-    gload(0);
-    lstore(0);
-    if (nsteps > 1) gload(1);
-    for (int s = 0; s < nsteps; ++s) {
+    gload(s0);
+    lstore(s0);
+    if (s0 + 1 < s1) gload(s0 + 1);
+    for (int s = s0; s < s1; ++s) {
       // this wave's stores of step s done; barrier: every wave's too, and step s-1's reads of the
       // other slot are finished
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (s + 1 < nsteps) lstore(s + 1);
-      if (s + 2 < nsteps) gload(s + 2);
+      if (s + 1 < s1) lstore(s + 1);
+      if (s + 2 < s1) gload(s + 2);
       const char* As = sm + (s & 1) * A_BYTES;
       const char* Bs = sm + B_OFF + (s & 1) * B_BYTES;
       half8 ah[TM], al[TM];
@@ -456,6 +460,21 @@ void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st
   HIP_OK(hipGetLastError());
 }
 
+// split-K combine: out = epilogue(sum over the nsplit partial planes, in split order)
+__global__ __launch_bounds__(256) void x4_split_reduce_kernel(ConvParams P, const float* __restrict__ part,
+                                                              int nsplit) {
+  const int HWo = P.Ho * P.Wo;
+  const int64_t n = (int64_t)P.B * P.Cout * HWo;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int p = (int)(i % HWo);
+  const int64_t r = i / HWo;
+  const int co = (int)(r % P.Cout), b = (int)(r / P.Cout);
+  float v = part[i];
+  for (int k = 1; k < nsplit; ++k) v += part[(int64_t)k * n + i];
+  conv_store(P, b, co, p, v);
+}
+
 // $MLIC_X4_RS=0: the LDS-DMA operand path (A/B switch); default the register-staged one
 static bool x4_rs() {
   static const bool on = [] {
@@ -466,39 +485,82 @@ static bool x4_rs() {
 }
 
 template <int K, int BM>
-static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st) {
+static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st,
+                      int nsplit) {
   int H, W;
   x4_grid(P, H, W);
   const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
-  dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B);
+  dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B * nsplit);
   static const int abl = [] {
     const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
     return e ? std::atoi(e) : 0;
   }();
   if (x4_rs())
-    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl);
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, nsplit);
   else
-    hipLaunchKernelGGL((conv_x4_kernel<K, BM, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl);
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, 1);
   HIP_OK(hipGetLastError());
 }
 
-void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st) {
+// split-K factor: a launch of few tiles per image (the latent-resolution 5x5 reprojections: 36 tiles
+// of one Cout tile, 1.1 waves of blocks over the CUs at 8 images) with a long K loop is cut into
+// nsplit K ranges whose partial sums a combine kernel adds in a fixed order.  A function of the
+// per-image shape only: the result bits must not depend on the batch (encoder = decoder).
+int x4_splitk(const ConvParams& P, int cin_pad) {
+  static const bool on = [] {  // $MLIC_X4_SPLITK=0: no split (A/B switch)
+    const char* e = std::getenv("MLIC_X4_SPLITK");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (!on || !x4_rs() || P.K == 1) return 1;
+  int H, W;
+  x4_grid(P, H, W);
+  const int tiles = ((P.Cout + x4_bm(P.Cout) - 1) / x4_bm(P.Cout)) * ((W + TC - 1) / TC) * ((H + TR - 1) / TR);
+  const int nsteps = cin_pad / 32 * P.K * P.K;
+  if (tiles > 48 || nsteps < 48) return 1;
+  return std::min(4, nsteps / 24);
+}
+
+int64_t x4_part_bytes(const ConvParams& P, int cin_pad) {
+  const int s = x4_splitk(P, cin_pad);
+  return s > 1 ? (int64_t)s * P.B * P.Cout * P.Ho * P.Wo * 4 : 0;
+}
+
+void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st,
+                     float* part) {
   MLIC_CHECK(conv_x4_ok(P, cin_pad) && act && wx, "conv_x4: unsupported shape");
   // the ConvParams input segments are not read: the packed copy (x4_pack_act) is
   ConvParams Q = P;
   Q.epi &= ~EPI_SQUARE_IN;
   const int nchunk = cin_pad / 32;
   const int bm = x4_bm(P.Cout);
-#define MLIC_X4_BM(K)                                              \
-  (bm == 256 ? launch_x4<K, 256>(Q, act, wx, nchunk, st)           \
-   : bm == 128 ? launch_x4<K, 128>(Q, act, wx, nchunk, st)         \
-               : launch_x4<K, 64>(Q, act, wx, nchunk, st))
+  const int nsplit = part ? x4_splitk(P, cin_pad) : 1;
+  ConvParams R = Q;  // the launch's view: the raw partial planes when split
+  if (nsplit > 1) {
+    R.epi = EPI_NONE;
+    R.bias = nullptr;
+    R.wexp = 0;
+    R.aux = nullptr;
+    R.res = nullptr;
+    R.out = part;
+    R.out_cs = (int64_t)P.Ho * P.Wo;
+    R.out_bs = (int64_t)P.Cout * R.out_cs;
+  }
+#define MLIC_X4_BM(K)                                                  \
+  (bm == 256 ? launch_x4<K, 256>(R, act, wx, nchunk, st, nsplit)       \
+   : bm == 128 ? launch_x4<K, 128>(R, act, wx, nchunk, st, nsplit)     \
+               : launch_x4<K, 64>(R, act, wx, nchunk, st, nsplit))
   switch (P.K) {
     case 1: MLIC_X4_BM(1); break;
     case 3: MLIC_X4_BM(3); break;
     default: MLIC_X4_BM(5); break;
   }
 #undef MLIC_X4_BM
+  if (nsplit > 1) {
+    const int64_t n = (int64_t)P.B * P.Cout * P.Ho * P.Wo;
+    hipLaunchKernelGGL(x4_split_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Q,
+                       (const float*)part, nsplit);
+    HIP_OK(hipGetLastError());
+  }
 }
 
 }  // namespace mlic

@@ -47,7 +47,11 @@ void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, i
 int64_t x4_act_halves(const ConvParams& P, int cin_pad);
 bool conv_x4_ok(const ConvParams& P, int cin_pad);
 void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st);
-void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st);
+// part: the split-K partial planes (x4_part_bytes bytes; nullptr = no split)
+int x4_splitk(const ConvParams& P, int cin_pad);
+int64_t x4_part_bytes(const ConvParams& P, int cin_pad);
+void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st,
+                     float* part = nullptr);
 
 // kernel-family selection (conv_dispatch.cpp)
 enum ConvImpl : int {
