@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "2")),
                     help="dense-conv arithmetic: 2 = split-fp16 MFMA v2 + specialised kernels, "
                          "1 = f16x3 v1 tiles, 0 = fp32 MFMA")
+    ap.add_argument("--synth-fp16", action="store_true",
+                    help="SURVEY 8(f)4: g_s subpel convs on fp16 operands with fp32 accumulation (x_hat within "
+                         "the 0.01 dB gate, bitstreams unchanged); default off: the headline stays fp32-faithful")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the profiled passes")
     ap.add_argument("--layers-out", default="", help="write the per-layer timing table here")
@@ -251,6 +254,7 @@ def main():
             n.update()
             n.set_lanes(a.lanes)
             n.set_precision(a.precision)
+            n.set_synthesis_precision(1 if a.synth_fp16 else 0)
             nets[(model, rate)] = n
     # inputs resident in HBM before the timed region
     xs = [torch.cat([synthetic.synth_image(j.H, j.W, j.seed) for j in js]).to(dev) for _, js in groups]
@@ -373,7 +377,8 @@ def main():
             "higher_is_better": True,
             "scaling": wl["scaling"],
             "vs_baseline": None,
-            "dtype": "f32" if a.precision == 0 else "f32 (dense convs: f32 via split-fp16 MFMA, 3 terms)",
+            "dtype": ("f32" if a.precision == 0 else "f32 (dense convs: f32 via split-fp16 MFMA, 3 terms)")
+                     + ("; g_s subpel convs fp16 operands, fp32 accumulate" if a.synth_fp16 else ""),
             "data": "synthetic (seeded sinusoid images; seeded conditioned realistic-rate weights)",
             "config": {"workload": wl["desc"] + " (full rANS bitstreams, inputs resident in HBM)",
                        "name": a.config, "model": wl["model"], "global_batch": n_jobs_total,
@@ -381,7 +386,8 @@ def main():
                        "shapes": sorted({f"{W}x{H}" for (_, _, H, W), _ in groups}),
                        "weights": ("high-rate set (round 1)" if cfg0[1] is None else
                                    f"rate set(s) {sorted({k[1] for k, _ in groups})} of synthetic.RATE_LAMBDAS"),
-                       "parallelism": f"image-sharded x{world} (no cross-GPU context)"},
+                       "parallelism": f"image-sharded x{world} (no cross-GPU context)",
+                       **({"synthesis": "fp16 operands (SURVEY f4)"} if a.synth_fp16 else {})},
             "roofline": roofline,
             **prof,
             "host_thread_ms_per_step": host,

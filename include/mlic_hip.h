@@ -81,6 +81,11 @@ int mlic_workspace_bytes(mlic_model* m, size_t* arena, size_t* weights);
 /* dense-conv arithmetic: 2 = split-fp16 MFMA "f16x3" v2 tiles + specialised kernels (default; error
  * below fp32 summation-order noise), 1 = f16x3 v1 tiles, 0 = fp32 MFMA.  Also $MLIC_PRECISION. */
 int mlic_set_precision(mlic_model* m, int precision);
+/* g_s only (synthesis.py:56-73): 0 = the model precision above (default), 1 = its dense
+ * subpel convs on fp16 operands with fp32 accumulation (one MFMA term instead of three).  Changes
+ * x_hat only (forward / decompress); bitstreams and likelihoods are unaffected.  Gate: |dPSNR| <= 0.01 dB.
+ * Also $MLIC_SYNTH_FP16=1. */
+int mlic_set_synthesis_precision(mlic_model* m, int mode);
 /* live kernel timing (HIP events on the executor stream), one category per kernel family / tile
  * instantiation: mlic_profile_categories gives the count, mlic_profile_category_name the kernel
  * name of each.  read() sums and clears. */
@@ -98,7 +103,8 @@ int mlic_profile_category_name(int cat, char* buf, size_t cap);
 /* kernel-level entry points (bit-exact tests, micro-benchmarks) */
 /* one conv layer with a given kernel family: impl -1 = the model's choice (precision 2), 0 fp32 MFMA,
  * 1 f16x3, 2 f16x3 v2, 3 resident-weight 1x1, 4 narrow 3x3, 5 small-Cin 1x1, 6 halo-tiled 3x3,
- * 7 x4 (split-fp16, both operands staged by LDS-DMA; K in 1, 3, 5, stride 1).  w is torch layout
+ * 7 x4 (split-fp16, both operands staged by LDS-DMA; K in 1, 3, 5, stride 1), 8 x4 with fp16 operands
+ * (single term, fp32 accumulation: the reduced-precision synthesis form).  w is torch layout
  * [Cout][Cin][K][K]; pad = K/2; epi = Epi flags of common.h (aux for GDN, res for residual).
  * Synchronous on `stream`. */
 int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const float* bias, float* y, int B, int Cin,

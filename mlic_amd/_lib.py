@@ -44,6 +44,7 @@ def _sig(lib):
         "mlic_set_profiling": [p, i],
         "mlic_set_lanes": [p, i],
         "mlic_set_precision": [p, i],
+        "mlic_set_synthesis_precision": [p, i],
         "mlic_profile_layers": [p, p, sz, P(sz)],
         "mlic_bench_conv": [i, i, i, i, i, i, i, i, i, i, P(C.c_double), P(C.c_double)],
         "mlic_profile_read": [p, i, P(i64), P(C.c_double), P(C.c_double), P(C.c_double)],

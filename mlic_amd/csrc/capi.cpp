@@ -63,6 +63,7 @@ int mlic_create(const char* model_name, int n, const char* const* names, const f
       m->impl = new Model(model_name, n, names, ptrs, shapes, ndims, (hipStream_t)stream);
       if (const char* e = std::getenv("MLIC_LANES")) m->impl->set_lanes(std::atoi(e));
       if (const char* e = std::getenv("MLIC_PRECISION")) m->impl->set_precision(std::atoi(e));
+      if (const char* e = std::getenv("MLIC_SYNTH_FP16")) m->impl->set_synthesis_precision(std::atoi(e) == 1 ? 1 : 0);
     } catch (...) {
       delete m;
       throw;
@@ -190,6 +191,13 @@ int mlic_set_precision(mlic_model* m, int precision) {
   return guard([&] {
     MLIC_CHECK(precision >= PREC_F32 && precision <= PREC_F16X3_V2, "precision must be 0 (f32), 1 or 2 (f16x3)");
     impl(m).set_precision(precision);
+  });
+}
+
+int mlic_set_synthesis_precision(mlic_model* m, int mode) {
+  return guard([&] {
+    MLIC_CHECK(mode == 0 || mode == 1, "synthesis precision must be 0 (fp32-faithful) or 1 (fp16 operands)");
+    impl(m).set_synthesis_precision(mode);
   });
 }
 
@@ -381,13 +389,19 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     MLIC_CHECK(!(epi & EPI_RES) || res, "residual epilogue needs res");
     P.aux = aux; P.aux_bs = (int64_t)Cout * Ho * Wo;
     P.res = res; P.res_bs = P.out_bs;
-    _Float16* wx = nullptr;
+    _Float16 *wx = nullptr, *wxh = nullptr;
     if (conv_x4_ok(P, cin_pad)) {
       HIP_OK(hipMallocAsync((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2, st));
       x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, st);
+      if (impl == CONV_X4H) {
+        HIP_OK(hipMallocAsync((void**)&wxh, x4_weight_halves(Cout, K * K, cin_pad, true) * 2, st));
+        x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wxh, st, true);
+      }
     }
-    const ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
+    ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
+    cw.wx4h = wxh;
     const int which = impl < 0 ? conv_select(P, cw, 2) : impl;
+    if (which == CONV_X4H) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
     if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
     if (which == CONV_NARROW) MLIC_CHECK(conv_narrow_ok(P), "narrow: unsupported shape");
     if (which == CONV_SMALLCIN) MLIC_CHECK(conv_smallcin_ok(P), "smallcin: unsupported shape");
@@ -399,6 +413,7 @@ int mlic_conv_run(void* stream, int impl, const float* x, const float* w, const 
     conv_run(which, P, cw, st, ws);
     if (ws) HIP_OK(hipFreeAsync(ws, st));
     if (wx) HIP_OK(hipFreeAsync(wx, st));
+    if (wxh) HIP_OK(hipFreeAsync(wxh, st));
     HIP_OK(hipFreeAsync(wp, st));
     HIP_OK(hipFreeAsync(wh, st));
     HIP_OK(hipFreeAsync(wl, st));

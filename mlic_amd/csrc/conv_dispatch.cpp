@@ -68,21 +68,25 @@ int conv_prof_cat(int impl, const ConvParams& P) {
     case CONV_PW: return PCAT_CONV_PW;
     case CONV_NARROW: return PCAT_CONV_NARROW;
     case CONV_HALO: return PCAT_CONV_HALO;
-    case CONV_X4: return PCAT_CONV_X4;
+    case CONV_X4:
+    case CONV_X4H: return PCAT_CONV_X4;
     default: return PCAT_CONV_SMALLCIN;
   }
 }
 
 int64_t conv_ws_bytes(int impl, const ConvParams& P, const ConvWeights& w) {
   // x4: the packed activations, then (256-byte aligned) the split-K partial planes
-  return impl == CONV_X4 ? (2 * x4_act_halves(P, w.cin_pad) + 255) / 256 * 256 + x4_part_bytes(P, w.cin_pad) : 0;
+  if (impl != CONV_X4 && impl != CONV_X4H) return 0;
+  const bool hi = impl == CONV_X4H;
+  return (2 * x4_act_halves(P, w.cin_pad, hi) + 255) / 256 * 256 + x4_part_bytes(P, w.cin_pad, hi);
 }
 
 void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t st, void* ws) {
   // the split-fp16 families read the prescaled hi/lo weights: their epilogues undo the row scale;
   // the fp32 families read the unscaled fp32 weights
   ConvParams P = P0;
-  const bool split = impl == CONV_X3 || impl == CONV_X3V2 || impl == CONV_PW || impl == CONV_HALO || impl == CONV_X4;
+  const bool split = impl == CONV_X3 || impl == CONV_X3V2 || impl == CONV_PW || impl == CONV_HALO || impl == CONV_X4 ||
+                     impl == CONV_X4H;
   P.wexp = split ? w.wexp : 0;
   switch (impl) {
     case CONV_F32: conv_forward(P, st); break;
@@ -92,13 +96,17 @@ void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t 
     case CONV_NARROW: conv_narrow_forward(P, st); break;
     case CONV_SMALLCIN: conv_smallcin_forward(P, st); break;
     case CONV_HALO: conv_halo_forward(P, w.wh, w.wl, w.cin_pad, st); break;
-    case CONV_X4: {
-      MLIC_CHECK(ws && w.wx4, "conv_x4: workspace and packed weights required");
+    case CONV_X4:
+    case CONV_X4H: {
+      const bool hi = impl == CONV_X4H;
+      const _Float16* wx = hi ? w.wx4h : w.wx4;
+      MLIC_CHECK(ws && wx, "conv_x4: workspace and packed weights required");
       _Float16* act = static_cast<_Float16*>(ws);
-      const int64_t abytes = (2 * x4_act_halves(P, w.cin_pad) + 255) / 256 * 256;
-      float* part = x4_part_bytes(P, w.cin_pad) > 0 ? reinterpret_cast<float*>(static_cast<char*>(ws) + abytes) : nullptr;
-      x4_pack_act(P, w.cin_pad, act, st);
-      conv_x4_forward(P, act, w.wx4, w.cin_pad, st, part);
+      const int64_t abytes = (2 * x4_act_halves(P, w.cin_pad, hi) + 255) / 256 * 256;
+      float* part = x4_part_bytes(P, w.cin_pad, hi) > 0 ? reinterpret_cast<float*>(static_cast<char*>(ws) + abytes)
+                                                         : nullptr;
+      x4_pack_act(P, w.cin_pad, act, st, hi);
+      conv_x4_forward(P, act, wx, w.cin_pad, st, part, hi);
       break;
     }
     default: throw Error("mlic: unknown conv implementation " + std::to_string(impl));

@@ -59,7 +59,10 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 // RS: register-staged operands (global_load_dwordx4 one step ahead, ds_write_b128 into a 2-slot
 // LDS ring) instead of LDS-DMA: a DMA piece costs ~100-185 issue cycles next to the ds_read/MFMA
 // stream (MI355X_MICROARCH.md), a dwordx4 load + ds_write_b128 pair a fraction of that
-template <int K, int BM, bool RS>
+// HI: the reduced-precision form (g_s only): rows hold the fp16 value of 64 channels
+// (granules 0-3: channels 0-31 of the chunk, 4-7: channels 32-63) and a K-step is 2 MFMAs per
+// fragment pair covering 64 channels: fp16 x fp16 products, fp32 accumulation
+template <int K, int BM, bool RS, bool HI>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
                                                       const _Float16* __restrict__ wx, int nchunk, int H, int W,
                                                       int abl, int nsplit) {
@@ -183,18 +186,28 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           bh[(j + 1) & 1] = lds_frag(Bs, n, G);
           bl[(j + 1) & 1] = lds_frag(Bs, n, G + 4);
         }
+        if constexpr (HI) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j & 1], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j & 1], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bl[j & 1], acc[i][j], 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j & 1], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j & 1], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
+        }
       }
     }
   } else {
+  static_assert(!HI, "the reduced-precision form runs on the register-staged path");
   // issue order: A0 B0 A1 | step 0: B1 A2 | step 1: B2 A3 | ...  Every step issues its NG DMA
   // instructions (past the end they re-fetch the last step into buffers no longer read), spread over
   // its pixel groups so the matrix pipe keeps running while the TA works through them.  At the top of
@@ -340,6 +353,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
 struct X4Pack {
   Seg seg[MAXSEG];
   int nseg, Cin, H, W, pad, nchunk, square, npix;  // npix: real pixels (K = 1 folds H*W into rows of 32)
+  int hi;  // reduced-precision layout: [hi of channels 0-31 | hi of channels 32-63] per 64-channel chunk
   _Float16* dst;
   int* rflag;
 };
@@ -353,23 +367,40 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   if (pos >= Hp * Wp) return;
   const int y = pos / Wp - Q.pad, x = pos % Wp - Q.pad;
   const bool inb = y >= 0 && y < Q.H && x >= 0 && x < Q.W && y * Q.W + x < Q.npix;
-  const int ch0 = cc * 32 + 8 * g;
-  int s = 0, c0 = 0;  // 8-channel groups never straddle a segment (segments are 16-aligned)
-  while (s + 1 < Q.nseg && ch0 >= c0 + Q.seg[s].C) { c0 += Q.seg[s].C; ++s; }
-  const Seg sg = Q.seg[s];
   const int64_t HW = Q.npix;  // channel plane stride of the (unfolded) input
-  const float* src = sg.p + (int64_t)b * sg.bs + (int64_t)(ch0 - c0) * HW + (int64_t)y * Q.W + x;
-  half8 h, l;
   bool bad = false;
+  // 8 consecutive channels from ch0 (8-channel groups never straddle a segment: segments are
+  // 16-aligned); out-of-range channels and border positions are zeros
+  auto load8 = [&](int ch0, float (&v)[8]) {
+    int s = 0, c0 = 0;
+    while (s + 1 < Q.nseg && ch0 >= c0 + Q.seg[s].C) { c0 += Q.seg[s].C; ++s; }
+    const Seg sg = Q.seg[s];
+    const float* src = sg.p + (int64_t)b * sg.bs + (int64_t)(ch0 - c0) * HW + (int64_t)y * Q.W + x;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool ok = inb && ch0 + j < Q.Cin && ch0 - c0 + j < sg.C;
-    float v = ok ? src[(int64_t)j * HW] : 0.0f;
-    if (Q.square) v *= v;
-    bad |= f16_unsafe(v);
-    const _Float16 hv = (_Float16)v;
-    h[j] = hv;
-    l[j] = (_Float16)(v - (float)hv);
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = inb && ch0 + j < Q.Cin && ch0 - c0 + j < sg.C;
+      v[j] = ok ? src[(int64_t)j * HW] : 0.0f;
+      if (Q.square) v[j] *= v[j];
+      bad |= f16_unsafe(v[j]);
+    }
+  };
+  half8 h, l;
+  float v[8];
+  if (Q.hi) {
+    load8(cc * 64 + 8 * g, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
+    load8(cc * 64 + 32 + 8 * g, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = (_Float16)v[j];
+  } else {
+    load8(cc * 32 + 8 * g, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const _Float16 hv = (_Float16)v[j];
+      h[j] = hv;
+      l[j] = (_Float16)(v[j] - (float)hv);
+    }
   }
   _Float16* d = Q.dst + (((int64_t)b * Q.nchunk + cc) * Hp * Wp + pos) * ROWH + 8 * g;
   *reinterpret_cast<half8*>(d) = h;
@@ -377,25 +408,28 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   range_report(Q.rflag, bad);
 }
 
-// weights: hi/lo [Cout][KK][cin_pad] -> [ct][step = chunk*KK + tap][BM rows][64 halves], swizzled
+// weights: hi/lo [Cout][KK][cin_pad] -> [ct][step = chunk*KK + tap][BM rows][64 halves], swizzled;
+// hi: the reduced-precision image, chunks of 64 channels of hi only (channels >= cin_pad are zeros)
 __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _Float16* __restrict__ wl,
                                        _Float16* __restrict__ dst, int Cout, int KK, int cin_pad, int BM,
-                                       int64_t n) {
+                                       int64_t n, int hi) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int e = (int)(i % ROWH);           // physical half within the row
   const int row = (int)((i / ROWH) % BM);
   const int64_t ts = i / ((int64_t)ROWH * BM);  // ct * nsteps + step
-  const int nchunk = cin_pad / 32, nsteps = nchunk * KK;
+  const int nchunk = hi ? (cin_pad + 63) / 64 : cin_pad / 32, nsteps = nchunk * KK;
   const int step = (int)(ts % nsteps), ct = (int)(ts / nsteps);
   const int cc = step / KK, tap = step - cc * KK;
   const int Gp = e >> 3, G = Gp ^ ((row >> 1) & 7);  // logical granule stored at physical Gp
-  const int k = (G & 3) * 8 + (e & 7);               // channel within the chunk
+  const int k = (G & 3) * 8 + (e & 7);               // channel within the 32-channel half
   const int co = ct * BM + row;
   _Float16 v = (_Float16)0.0f;
   if (co < Cout) {
-    const int64_t off = ((int64_t)co * KK + tap) * cin_pad + cc * 32 + k;
-    v = G < 4 ? wh[off] : wl[off];
+    const int ch = hi ? cc * 64 + (G >> 2) * 32 + k : cc * 32 + k;
+    const int64_t off = ((int64_t)co * KK + tap) * cin_pad + ch;
+    if (hi) v = ch < cin_pad ? wh[off] : (_Float16)0.0f;
+    else v = G < 4 ? wh[off] : wl[off];
   }
   dst[i] = v;
 }
@@ -408,19 +442,20 @@ int x4_bm(int Cout) {
   return (Cout >= 192 && 8 * (w256 - w128) <= Cout) ? 256 : 128;
 }
 
-int64_t x4_weight_halves(int Cout, int KK, int cin_pad) {
+int x4_nchunk(int cin_pad, bool hi) { return hi ? (cin_pad + 63) / 64 : cin_pad / 32; }
+
+int64_t x4_weight_halves(int Cout, int KK, int cin_pad, bool hi) {
   const int bm = x4_bm(Cout);
-  return (int64_t)((Cout + bm - 1) / bm) * bm * KK * (cin_pad / 32) * ROWH;
+  return (int64_t)((Cout + bm - 1) / bm) * bm * KK * x4_nchunk(cin_pad, hi) * ROWH;
 }
 
 void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, int cin_pad, _Float16* dst,
-                     hipStream_t st) {
-  const int64_t n = x4_weight_halves(Cout, KK, cin_pad);
+                     hipStream_t st, bool hi) {
+  const int64_t n = x4_weight_halves(Cout, KK, cin_pad, hi);
   hipLaunchKernelGGL(x4_pack_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wh, wl, dst, Cout,
-                     KK, cin_pad, x4_bm(Cout), n);
+                     KK, cin_pad, x4_bm(Cout), n, hi ? 1 : 0);
   HIP_OK(hipGetLastError());
 }
-
 // K = 1: no spatial coupling, so the flat pixel index is folded into rows of TC = 32: every
 // 8 x 32 tile is 256 consecutive pixels and only the image's last tile is ragged
 static void x4_grid(const ConvParams& P, int& H, int& W) {
@@ -428,11 +463,11 @@ static void x4_grid(const ConvParams& P, int& H, int& W) {
   W = P.K == 1 ? TC : P.W;
 }
 
-int64_t x4_act_halves(const ConvParams& P, int cin_pad) {
+int64_t x4_act_halves(const ConvParams& P, int cin_pad, bool hi) {
   const int pad = P.K / 2;
   int H, W;
   x4_grid(P, H, W);
-  return (int64_t)P.B * (cin_pad / 32) * (H + 2 * pad) * (W + 2 * pad) * ROWH;
+  return (int64_t)P.B * x4_nchunk(cin_pad, hi) * (H + 2 * pad) * (W + 2 * pad) * ROWH;
 }
 
 bool conv_x4_ok(const ConvParams& P, int cin_pad) {
@@ -443,7 +478,7 @@ bool conv_x4_ok(const ConvParams& P, int cin_pad) {
   return true;
 }
 
-void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st) {
+void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st, bool hi) {
   X4Pack Q{};
   for (int s = 0; s < P.nseg; ++s) Q.seg[s] = P.seg[s];
   Q.nseg = P.nseg;
@@ -451,7 +486,8 @@ void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st
   x4_grid(P, Q.H, Q.W);
   Q.npix = P.H * P.W;
   Q.pad = P.K / 2;
-  Q.nchunk = cin_pad / 32;
+  Q.nchunk = x4_nchunk(cin_pad, hi);
+  Q.hi = hi ? 1 : 0;
   Q.square = (P.epi & EPI_SQUARE_IN) ? 1 : 0;
   Q.dst = dst;
   Q.rflag = P.rflag;
@@ -486,7 +522,7 @@ static bool x4_rs() {
 
 template <int K, int BM>
 static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st,
-                      int nsplit) {
+                      int nsplit, bool hi) {
   int H, W;
   x4_grid(P, H, W);
   const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
@@ -495,10 +531,14 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
     const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
     return e ? std::atoi(e) : 0;
   }();
-  if (x4_rs())
-    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, nsplit);
+  if (hi)
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
+                       nsplit);
+  else if (x4_rs())
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
+                       nsplit);
   else
-    hipLaunchKernelGGL((conv_x4_kernel<K, BM, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, 1);
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, false, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, 1);
   HIP_OK(hipGetLastError());
 }
 
@@ -506,7 +546,7 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
 // of one Cout tile, 1.1 waves of blocks over the CUs at 8 images) with a long K loop is cut into
 // nsplit K ranges whose partial sums a combine kernel adds in a fixed order.  A function of the
 // per-image shape only: the result bits must not depend on the batch (encoder = decoder).
-int x4_splitk(const ConvParams& P, int cin_pad) {
+int x4_splitk(const ConvParams& P, int cin_pad, bool hi) {
   static const bool on = [] {  // $MLIC_X4_SPLITK=0: no split (A/B switch)
     const char* e = std::getenv("MLIC_X4_SPLITK");
     return !(e && std::atoi(e) == 0);
@@ -515,25 +555,25 @@ int x4_splitk(const ConvParams& P, int cin_pad) {
   int H, W;
   x4_grid(P, H, W);
   const int tiles = ((P.Cout + x4_bm(P.Cout) - 1) / x4_bm(P.Cout)) * ((W + TC - 1) / TC) * ((H + TR - 1) / TR);
-  const int nsteps = cin_pad / 32 * P.K * P.K;
+  const int nsteps = x4_nchunk(cin_pad, hi) * P.K * P.K;
   if (tiles > 48 || nsteps < 48) return 1;
   return std::min(4, nsteps / 24);
 }
 
-int64_t x4_part_bytes(const ConvParams& P, int cin_pad) {
-  const int s = x4_splitk(P, cin_pad);
+int64_t x4_part_bytes(const ConvParams& P, int cin_pad, bool hi) {
+  const int s = x4_splitk(P, cin_pad, hi);
   return s > 1 ? (int64_t)s * P.B * P.Cout * P.Ho * P.Wo * 4 : 0;
 }
 
 void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st,
-                     float* part) {
+                     float* part, bool hi) {
   MLIC_CHECK(conv_x4_ok(P, cin_pad) && act && wx, "conv_x4: unsupported shape");
   // the ConvParams input segments are not read: the packed copy (x4_pack_act) is
   ConvParams Q = P;
   Q.epi &= ~EPI_SQUARE_IN;
-  const int nchunk = cin_pad / 32;
+  const int nchunk = x4_nchunk(cin_pad, hi);
   const int bm = x4_bm(P.Cout);
-  const int nsplit = part ? x4_splitk(P, cin_pad) : 1;
+  const int nsplit = part ? x4_splitk(P, cin_pad, hi) : 1;
   ConvParams R = Q;  // the launch's view: the raw partial planes when split
   if (nsplit > 1) {
     R.epi = EPI_NONE;
@@ -546,9 +586,9 @@ void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* w
     R.out_bs = (int64_t)P.Cout * R.out_cs;
   }
 #define MLIC_X4_BM(K)                                                  \
-  (bm == 256 ? launch_x4<K, 256>(R, act, wx, nchunk, st, nsplit)       \
-   : bm == 128 ? launch_x4<K, 128>(R, act, wx, nchunk, st, nsplit)     \
-               : launch_x4<K, 64>(R, act, wx, nchunk, st, nsplit))
+  (bm == 256 ? launch_x4<K, 256>(R, act, wx, nchunk, st, nsplit, hi)       \
+   : bm == 128 ? launch_x4<K, 128>(R, act, wx, nchunk, st, nsplit, hi)     \
+               : launch_x4<K, 64>(R, act, wx, nchunk, st, nsplit, hi))
   switch (P.K) {
     case 1: MLIC_X4_BM(1); break;
     case 3: MLIC_X4_BM(3); break;

@@ -41,22 +41,25 @@ void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, i
 // LDS-DMA split-fp16 conv (conv_x4.hip): activations packed per call into a zero-bordered split
 // layout (x4_pack_act, workspace of x4_act_halves halves), weights packed once (x4_pack_weights)
 int x4_bm(int Cout);
-int64_t x4_weight_halves(int Cout, int KK, int cin_pad);
+// hi = the reduced-precision form (single fp16 term, 64-channel chunks; g_s only)
+int x4_nchunk(int cin_pad, bool hi);
+int64_t x4_weight_halves(int Cout, int KK, int cin_pad, bool hi = false);
 void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, int cin_pad, _Float16* dst,
-                     hipStream_t st);
-int64_t x4_act_halves(const ConvParams& P, int cin_pad);
+                     hipStream_t st, bool hi = false);
+int64_t x4_act_halves(const ConvParams& P, int cin_pad, bool hi = false);
 bool conv_x4_ok(const ConvParams& P, int cin_pad);
-void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st);
+void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st, bool hi = false);
 // part: the split-K partial planes (x4_part_bytes bytes; nullptr = no split)
-int x4_splitk(const ConvParams& P, int cin_pad);
-int64_t x4_part_bytes(const ConvParams& P, int cin_pad);
+int x4_splitk(const ConvParams& P, int cin_pad, bool hi = false);
+int64_t x4_part_bytes(const ConvParams& P, int cin_pad, bool hi = false);
 void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st,
-                     float* part = nullptr);
+                     float* part = nullptr, bool hi = false);
 
 // kernel-family selection (conv_dispatch.cpp)
 enum ConvImpl : int {
   CONV_F32 = 0, CONV_X3 = 1, CONV_X3V2 = 2, CONV_PW = 3, CONV_NARROW = 4, CONV_SMALLCIN = 5, CONV_HALO = 6,
-  CONV_X4 = 7
+  CONV_X4 = 7,
+  CONV_X4H = 8  // x4 in the reduced-precision form (fp16 operands, fp32 accumulation): g_s on request only
 };
 struct ConvWeights {
   const float* wpk;  // fp32 packed [K*K][Cin][Cout] (in ConvParams too)
@@ -65,6 +68,7 @@ struct ConvWeights {
   int cin_pad;
   const _Float16* wx4 = nullptr;  // x4_pack_weights image (null: CONV_X4 not available)
   int wexp = 0;                   // wh/wl hold w * 2^wexp (split_weights)
+  const _Float16* wx4h = nullptr; // the reduced-precision image (x4_pack_weights hi; null: no CONV_X4H)
 };
 int conv_select(const ConvParams& P, const ConvWeights& w, int precision);
 // device workspace conv_run needs for impl (bytes; 0 = none)

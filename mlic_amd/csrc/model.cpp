@@ -12,6 +12,12 @@
 
 namespace mlic {
 
+// g_s's dense 3x3 subpel convs (ResidualBlockUpsample subpel_conv / upsample, res_blk.py:107,111):
+// the convs the reduced-precision synthesis mode runs in the single-term fp16 form
+static bool gs_subpel(const std::string& name, const ConvW& w) {
+  return name.rfind("g_s.", 0) == 0 && w.K == 3 && w.wh != nullptr;
+}
+
 // ------------------------------------------------------------------------------------- configs
 Cfg config_for(const std::string& name) {  // config/config.py:19-62 (+ MLICPP_L_VBR)
   Cfg c;
@@ -186,8 +192,10 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     int64_t nx = 0;
     for (auto& kv : convs_) {
       const ConvW& w = kv.second;
-      if (w.wh && (w.K == 1 || w.K == 3 || w.K == 5) && w.Cout >= 64)
+      if (w.wh && (w.K == 1 || w.K == 3 || w.K == 5) && w.Cout >= 64) {
         nx += (x4_weight_halves(w.Cout, w.K * w.K, w.cin_pad) + 127) & ~(int64_t)127;
+        if (gs_subpel(kv.first, w)) nx += (x4_weight_halves(w.Cout, w.K * w.K, w.cin_pad, true) + 127) & ~(int64_t)127;
+      }
     }
     if (nx > 0) {
       _Float16* xb = nullptr;
@@ -201,6 +209,11 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
         w.wx4 = xb + xo;
         x4_pack_weights(w.wh, w.wl, w.Cout, w.K * w.K, w.cin_pad, w.wx4, st);
         xo += (x4_weight_halves(w.Cout, w.K * w.K, w.cin_pad) + 127) & ~(int64_t)127;
+        if (gs_subpel(kv.first, w)) {
+          w.wx4h = xb + xo;
+          x4_pack_weights(w.wh, w.wl, w.Cout, w.K * w.K, w.cin_pad, w.wx4h, st, true);
+          xo += (x4_weight_halves(w.Cout, w.K * w.K, w.cin_pad, true) + 127) & ~(int64_t)127;
+        }
       }
     }
   }
@@ -513,19 +526,21 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
     run_conv(P2, w2, nullptr);
     return;
   }
+  // the reduced-precision form when requested (set_synthesis_precision(1)) and both images exist
+  const bool hi = gs_fp16_ && w1.wx4h && w2.wx4h;
   const size_t m = L().arena.mark();
-  _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((conv_ws_bytes(CONV_X4, P1, c1) + 3) / 4));
-  timed(PCAT_ELEM, 0.0, 8.0 * L().B * P1.Cin * P1.H * P1.W, [&] { x4_pack_act(P1, w1.cin_pad, act, L().st); },
-        w1.name + ".__x4_pack");
-  run_conv(P1, w1, act);
-  run_conv(P2, w2, act);
+  _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((conv_ws_bytes(hi ? CONV_X4H : CONV_X4, P1, c1) + 3) / 4));
+  timed(PCAT_ELEM, 0.0, (hi ? 6.0 : 8.0) * L().B * P1.Cin * P1.H * P1.W,
+        [&] { x4_pack_act(P1, w1.cin_pad, act, L().st, hi); }, w1.name + ".__x4_pack");
+  run_conv(P1, w1, act, hi);
+  run_conv(P2, w2, act, hi);
   L().arena.release(m);
 }
 
 // packed: the input already in x4's split layout (conv_pair); the impl is then necessarily x4
-void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed) {
+void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi) {
   const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4, w.wexp};
-  const int impl = packed ? CONV_X4 : conv_select(P, cw, precision_);
+  const int impl = packed ? (hi ? CONV_X4H : CONV_X4) : conv_select(P, cw, precision_);
   const double outn = (double)P.B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * P.Cin * w.K * w.K;
   const double bytes = 4.0 * ((double)P.B * P.Cin * P.H * P.W + (double)w.Cout * P.Cin * w.K * w.K +
@@ -538,7 +553,8 @@ void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed
     tag = w.name + sh;
   }
   if (packed) {
-    timed(conv_prof_cat(impl, P), flops, bytes, [&] { conv_x4_forward(P, packed, w.wx4, w.cin_pad, L().st); }, tag);
+    timed(conv_prof_cat(impl, P), flops, bytes,
+          [&] { conv_x4_forward(P, packed, hi ? w.wx4h : w.wx4, w.cin_pad, L().st, nullptr, hi); }, tag);
     return;
   }
   const int64_t wsb = conv_ws_bytes(impl, P, cw);

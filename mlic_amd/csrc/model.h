@@ -32,6 +32,7 @@ struct ConvW {
   _Float16* wl = nullptr;
   int cin_pad = 0;
   _Float16* wx4 = nullptr;   // x4 LDS-image weights [ct][step][BM][64]     (conv_x4 path)
+  _Float16* wx4h = nullptr;  // reduced-precision x4 image (64 channels of hi per row; g_s subpel convs)
   int wexp = 0;              // wh/wl hold w * 2^wexp (exact layer prescale, split_weights)
   std::string name;          // state_dict prefix (profiling)
 };
@@ -157,6 +158,10 @@ class Model {
   void set_lanes(int n);
   void set_precision(int p) { precision_ = p; }
   int precision() const { return precision_; }
+  // g_s's dense subpel convs: 0 = fp32-faithful (the model precision), 1 = fp16 operands with fp32
+  // accumulation (decoder output only: bitstreams and likelihoods do not change)
+  void set_synthesis_precision(int p) { gs_fp16_ = p == 1; }
+  int synthesis_precision() const { return gs_fp16_ ? 1 : 0; }
   int lanes() const { return nlanes_; }
   ProfStat profile_read(int cat);  // synchronises the recorded events; clears that category
   std::string profile_layers();     // per-tag table of the recorded events (does not clear)
@@ -198,6 +203,7 @@ class Model {
   std::vector<std::unique_ptr<Lane>> lanes_;
   int nlanes_ = 4;
   int precision_ = PREC_F16X3_V2;
+  bool gs_fp16_ = false;
   HostStats hstats_;
   bool prof_ = false;
   static thread_local Lane* tl_lane_;
@@ -225,7 +231,7 @@ class Model {
             const View* aux = nullptr, const View* res = nullptr);
   ConvParams conv_params(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
                          const View* aux, const View* res);
-  void run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed);
+  void run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi = false);
   void add_fusion_x4(const std::string& base, const float* w_dev, int Cout, hipStream_t st);
   void conv_pair(const std::vector<View>& ins, const ConvW& w1, const View& out1, int epi1, const ConvW& w2,
                  const View& out2, int epi2);

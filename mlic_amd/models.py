@@ -149,6 +149,8 @@ class MLICPlusPlus(nn.Module):
             _lib.call("mlic_set_lanes", h, self._lanes)
         if getattr(self, "_precision", None) is not None:
             _lib.call("mlic_set_precision", h, self._precision)
+        if getattr(self, "_synth_precision", None) is not None:
+            _lib.call("mlic_set_synthesis_precision", h, self._synth_precision)
         return h
 
     def _vbr_scales(self, B: int, **kw) -> np.ndarray:
@@ -156,10 +158,17 @@ class MLICPlusPlus(nn.Module):
         return np.ones(B, np.float32)
 
     def set_precision(self, mode: int):
-        """Dense-conv arithmetic: 1 = split-fp16 MFMA "f16x3" (default), 0 = fp32 MFMA."""
+        """Dense-conv arithmetic: 2 = split-fp16 MFMA "f16x3" (default), 0 = fp32 MFMA."""
         self._precision = int(mode)
         if self._handle is not None:
             _lib.call("mlic_set_precision", self._handle, self._precision)
+
+    def set_synthesis_precision(self, mode: int):
+        """g_s only (synthesis.py:56-73): 0 = the model precision (default), 1 = its dense subpel convs on
+        fp16 operands with fp32 accumulation.  x_hat changes within the 0.01 dB gate; bitstreams do not."""
+        self._synth_precision = int(mode)
+        if self._handle is not None:
+            _lib.call("mlic_set_synthesis_precision", self._handle, self._synth_precision)
 
     def set_lanes(self, n: int):
         """Host threads x HIP streams used by compress()/decompress() (results do not depend on it)."""

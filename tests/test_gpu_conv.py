@@ -12,7 +12,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 GELU, GDN, IGDN, TANH, MASK_A, MASK_N, RES, SHUFFLE, SQUARE = 1, 2, 4, 8, 16, 32, 64, 128, 256
-F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, X4, AUTO = 0, 1, 2, 3, 4, 5, 6, 7, -1
+F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, X4, X4H, AUTO = 0, 1, 2, 3, 4, 5, 6, 7, 8, -1
 
 
 def reference(x, w, b, stride, epi, res):
@@ -173,6 +173,40 @@ def test_halo_k1_k5(shape):
 def test_x4(shape):
     B, cin, cout, H, W, K, epi = shape
     check(*run(X4, B, cin, cout, H, W, K, epi=epi))
+
+
+def _fp16_operands(x, w):
+    """The operands the reduced-precision x4 form multiplies: x rounded to fp16, w rounded to fp16
+    after the layer's exact power-of-two prescale (max |w| * 2^e in [2^14, 2^15), split_weights)."""
+    e = 14 - math.floor(math.log2(w.abs().max().item()))
+    return x.half().double(), (w * 2.0 ** e).half().double() / 2.0 ** e
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 192, 768, 24, 64, 3, SHUFFLE | GELU),   # g_s subpel conv (MLICPP_L): 3 chunks of 64 channels
+    (1, 192, 768, 19, 45, 3, SHUFFLE),          # ragged pixel tiles at every edge
+    (1, 96, 384, 16, 40, 3, SHUFFLE | GELU),    # MLICPP_S width: 96 channels = one zero-padded chunk pair
+    (1, 100, 200, 9, 33, 3, RES),               # Cin not a multiple of 32, partial Cout tile, residual
+    (1, 320, 64, 13, 37, 5, 0),                 # 5x5 with few tiles: the split-K path
+])
+def test_x4_fp16_operands(shape):
+    """The reduced-precision synthesis form: fp16 x fp16 products with fp32 accumulation.
+    Against float64 of the fp16-rounded operands it is exact to fp32 summation noise (2e-5), and
+    against the fp32 conv it is within fp16 operand rounding (2e-3 of the output scale)."""
+    from mlic_amd import _lib
+    B, cin, cout, H, W, K, epi = shape
+    y, ref = run(X4H, B, cin, cout, H, W, K, epi=epi)
+    check(y, ref, rtol=2e-3)
+    g = torch.Generator().manual_seed(0)  # run()'s operands, regenerated
+    dev = torch.device("cuda")
+    x = (torch.rand(B, cin, H, W, generator=g) - 0.5).to(dev)
+    w = ((torch.rand(cout, cin, K, K, generator=g) - 0.5) / (cin * K * K) ** 0.5).to(dev)
+    b = (torch.rand(cout, generator=g) - 0.5).to(dev)
+    oshape = (B, cout // 4, 2 * H, 2 * W) if epi & SHUFFLE else (B, cout, H, W)
+    res = (torch.rand(*oshape, generator=g) - 0.5).to(dev) if epi & RES else None
+    xh, wh = _fp16_operands(x.double(), w.double())
+    ref16 = reference(xh, wh, b.double(), 1, epi, res.double() if res is not None else None).float()
+    check(y, ref16, rtol=2e-5)
 
 
 def test_x4_auto_selection():

@@ -521,3 +521,40 @@ def test_fp16_range_guard():
     net.update()
     with pytest.raises(_lib.MlicError, match="fp16 range"):
         net.compress(x)
+
+
+@pytest.mark.parametrize("name,rate,H,W", [("MLICPP_L", 2, 1088, 1920), ("MLICPP_S", 2, 512, 768),
+                                           ("MLICPP_M_SMALL_DEC", 2, 256, 384)])
+def test_synthesis_fp16_gate(name, rate, H, W):
+    """SURVEY 8(f)4, reduced-precision g_s (synthesis.py:56-73): its dense subpel convs on fp16
+    operands with fp32 accumulation.  The gate is BASELINE's |dPSNR| <= 0.01 dB, checked two ways:
+    on the uint8 PSNR of this run, and as an operating-point-free bound -- the RMS change of x_hat
+    must stay below 8.5e-4, which moves the PSNR of a codec at 35 dB (MSE 3.2e-4, the reference's
+    high end, results/kodak) by <= 0.01 dB.  Likelihoods and bitstreams must not change at all."""
+    net = rate_net(name, rate)
+    net.update()
+    x = synthetic.synth_image(H, W, 11).to(DEV)
+    f32 = net(x)
+    c32 = net.compress(x)
+    try:
+        net.set_synthesis_precision(1)
+        f16 = net(x)
+        c16 = net.compress(x)
+        d16 = net.decompress(c16["strings"], c16["shape"])
+    finally:
+        net.set_synthesis_precision(0)
+    torch.cuda.synchronize()
+    for k in ("y_likelihoods", "z_likelihoods"):
+        assert torch.equal(f16["likelihoods"][k], f32["likelihoods"][k]), k
+    assert c16["strings"] == c32["strings"]
+    assert torch.equal(d16["x_hat"], f16["x_hat"])
+    xc = x.cpu()
+    p32, p16 = ref.psnr_uint8(xc, f32["x_hat"].cpu()), ref.psnr_uint8(xc, f16["x_hat"].cpu())
+    d = (f16["x_hat"].double() - f32["x_hat"].double())
+    rms = float(d.pow(2).mean().sqrt())
+    rec = {"psnr_fp32": p32, "psnr_fp16_gs": p16, "dpsnr_db": p16 - p32, "xhat_rms_change": rms,
+           "xhat_max_change": float(d.abs().max()),
+           "dpsnr_at_35db_bound": 10 * math.log10(1 + rms ** 2 / 10 ** -3.5)}
+    PARITY[f"synth_fp16_{name}_{H}x{W}"] = rec
+    assert abs(p16 - p32) <= 0.01, rec
+    assert rms <= 8.5e-4, rec
