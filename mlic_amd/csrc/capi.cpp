@@ -279,13 +279,19 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
       P.res = y;
       P.res_bs = P.out_bs;
     }
-    _Float16* wx = nullptr;
+    _Float16 *wx = nullptr, *wxh = nullptr;
     if (conv_x4_ok(P, cin_pad)) {
       HIP_OK(hipMalloc((void**)&wx, x4_weight_halves(Cout, K * K, cin_pad) * 2));
       x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wx, nullptr);
+      if (impl == CONV_X4H) {
+        HIP_OK(hipMalloc((void**)&wxh, x4_weight_halves(Cout, K * K, cin_pad, true) * 2));
+        x4_pack_weights(wh, wl, Cout, K * K, cin_pad, wxh, nullptr, true);
+      }
     }
-    const ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
+    ConvWeights cw{wp, wh, wl, cin_pad, wx, wexp};
+    cw.wx4h = wxh;
     const int which = impl < 0 ? conv_select(P, cw, 2) : impl;  // < 0: what the model runs (precision 2)
+    if (which == CONV_X4H) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
     if (which == CONV_PW) MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
     if (which == CONV_X4) MLIC_CHECK(conv_x4_ok(P, cin_pad), "x4: unsupported shape");
     void* ws = nullptr;
@@ -307,7 +313,7 @@ int mlic_bench_conv(int impl, int B, int Cin, int Cout, int H, int W, int K, int
     *tflops = 2.0 * (double)B * Cout * Ho * Wo * Cin * K * K / (*ms_per * 1e-3) / 1e12;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl, (void*)wx, ws})
+    for (void* p : {(void*)x, (void*)y, (void*)w, (void*)wp, (void*)bias, (void*)wh, (void*)wl, (void*)wx, (void*)wxh, ws})
       if (p) (void)hipFree(p);
   });
 }

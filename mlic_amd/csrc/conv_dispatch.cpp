@@ -39,15 +39,20 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if (precision == 1) return CONV_X3;
   // resident weights pay once the grid fills the chip: >= 4 K pixels per image
   if ((int64_t)P.Ho * P.Wo >= 4096 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
-  // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs), and the big 1x1 GEMMs (the
-  // hoisted EntropyParameters hyper columns, h_s's last layer: Cin x Cout >= 2^18; smaller 1x1s
-  // measured even or slower than x3v2), once the grid fills the chip
-  const bool x4_shape = P.K == 1 ? (int64_t)P.Cin * P.Cout >= (1 << 18) : P.Cout >= (P.K == 3 ? 192 : 64);
+  // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs), the 5x5 reprojections, the big
+  // 1x1 GEMMs (the hoisted EntropyParameters hyper columns, h_s's last layer: Cin x Cout >= 2^18) and
+  // the mid-size latent 1x1s with 192 <= Cin <= 352 < ... (context q/k/v 224..288, LRP of slice 0:
+  // 1.1-1.3x x3v2; the LRP's wider inputs, 384..640 -> 224, stay on x3v2, 1.1x faster there).  3x3
+  // and 5x5 take any grid: the split-K path (x4_splitk) fills the chip for few-tile shapes (h_s at the
+  // z grid, 8 x 12 .. 17 x 30: 1.5-2.5x x3v2); K = 1 has no split and needs >= 32 tiles per image
+  const bool x4_shape = P.K == 1 ? ((int64_t)P.Cin * P.Cout >= (1 << 18) ||
+                                    (P.Cin >= 192 && P.Cin <= 352 && P.Cout >= 192))
+                                 : P.Cout >= (P.K == 3 ? 192 : 64);
   if (w.wx4 && x4_on() && x4_k_on(P.K) && x4_shape && conv_x4_ok(P, w.cin_pad)) {
+    if (P.K != 1) return CONV_X4;
     const int bm = x4_bm(P.Cout);
-    const int64_t rows = P.K == 1 ? ((int64_t)P.H * P.W + 31) / 32 : P.H;
-    const int64_t cols = P.K == 1 ? 1 : (P.W + 31) / 32;
-    if ((int64_t)((P.Cout + bm - 1) / bm) * cols * ((rows + 7) / 8) >= 32) return CONV_X4;
+    const int64_t rows = ((int64_t)P.H * P.W + 31) / 32;
+    if ((int64_t)((P.Cout + bm - 1) / bm) * ((rows + 7) / 8) >= 32) return CONV_X4;
   }
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay

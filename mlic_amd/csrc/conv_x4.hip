@@ -58,7 +58,9 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 
 // RS: register-staged operands (global_load_dwordx4 one step ahead, ds_write_b128 into a 2-slot
 // LDS ring) instead of LDS-DMA: a DMA piece costs ~100-185 issue cycles next to the ds_read/MFMA
-// stream (MI355X_MICROARCH.md), a dwordx4 load + ds_write_b128 pair a fraction of that
+// stream (MI355X_MICROARCH.md), a dwordx4 load + ds_write_b128 pair a fraction of that.  (Measured:
+// A fragments loaded fragment-shaped straight into registers, skipping LDS, ran 2-15 % slower on
+// every bench shape -- twice the VMEM instructions for the same bytes.)
 // HI: the reduced-precision form (g_s only): rows hold the fp16 value of 64 channels
 // (granules 0-3: channels 0-31 of the chunk, 4-7: channels 32-63) and a K-step is 2 MFMAs per
 // fragment pair covering 64 channels: fp16 x fp16 products, fp32 accumulation
