@@ -151,7 +151,7 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_mfma_kernel(LocalAttnPa
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
-      s[r] = j < 25 ? expf(s[r] - mx) : 0.0f;
+      s[r] = j < 25 ? softmax_exp(s[r] - mx) : 0.0f;
       sum += s[r];
     }
     sum += __shfl_xor(sum, 32);
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
       float sum = 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sacc[hh][r] = ((jbits >> r) & 1u) ? expf(sacc[hh][r] - mx) : 0.0f;
+        sacc[hh][r] = ((jbits >> r) & 1u) ? softmax_exp(sacc[hh][r] - mx) : 0.0f;
         sum += sacc[hh][r];
       }
       sum += __shfl_xor(sum, 32);

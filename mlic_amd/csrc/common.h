@@ -94,6 +94,12 @@ struct ConvParams {
 // rounds to inf; NaN included) is noted in a per-thread bit, and range_report raises *flag once per
 // thread at the end of the kernel; the executor then re-runs forward on the exact fp32 MFMA path, or
 // fails compress/decompress loudly (Model::range_hit / range_fail)
+// softmax exponent on the hardware exp2 (one v_exp_f32 + one multiply instead of expf's ~12-instruction
+// range-reduced sequence): e^x = 2^(x log2 e).  Arguments are x - max <= 0; relative error
+// <= 1 ulp + |x| 2^-24 ln 2 (1e-7 at |x| = 1, 1e-6 at |x| = 20, where e^x < 3e-9 of the largest term).
+// Encoder and decoder run the same kernels, so bit-reproducibility is unaffected.
+__device__ __forceinline__ float softmax_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
 __device__ __forceinline__ bool f16_unsafe(float v) { return (__float_as_uint(v) & 0x7fffffffu) >= 0x477ff000u; }
 __device__ __forceinline__ void range_report(int* flag, bool bad) {
   if (bad && flag) atomicOr(flag, 1);

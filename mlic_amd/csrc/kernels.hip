@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void local_attn_kernel(LocalAttnParams P) {
     }
     float sum = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 25; ++j) { sc[j] = expf(sc[j] - mx); sum += sc[j]; }
+    for (int j = 0; j < 25; ++j) { sc[j] = softmax_exp(sc[j] - mx); sum += sc[j]; }
     const float inv = 1.0f / sum;
 #pragma unroll
     for (int j = 0; j < 25; ++j) sc[j] = sc[j] * inv;
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void ctx_partial_kernel(const float* __restric
     }
 #pragma unroll
     for (int j = 0; j < NE; ++j) {
-      const float e = on ? expf(kv[j] - mloc[j]) : 0.0f;
+      const float e = on ? softmax_exp(kv[j] - mloc[j]) : 0.0f;
       ssum[j] += e;
       kt[lane][wave + 4 * j] = e;
       vt[lane][wave + 4 * j] = vv[j];
@@ -522,7 +522,7 @@ __global__ void ctx_reduce_kernel(const float* __restrict__ part, float* __restr
   float num = 0.0f, den = 0.0f;
   for (int k = 0; k < nsplit; ++k) {
     const float* r = src + (int64_t)k * rec;
-    const float w = expf(r[c] - M);
+    const float w = softmax_exp(r[c] - M);
     num = fmaf(w, r[hd + o], num);
     den = fmaf(w, r[hd + nout + c], den);
   }
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256) void attn_apply_kernel(const float* __restrict
   float sum = 0.0f;
 #pragma unroll
   for (int c = 0; c < hd; ++c) {
-    q[c] = expf(q[c] - mx);
+    q[c] = softmax_exp(q[c] - mx);
     sum += q[c];
   }
   const float inv = 1.0f / sum;
