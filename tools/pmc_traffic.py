@@ -38,6 +38,13 @@ def main():
                # (this kernel's operand loads are 16-B/lane) -> doubled; WRITE_SIZE is exact
                conv_hbm_bytes_per_launch=(2 * f + w) if f is not None and w is not None else None,
                conv_hbm_bytes_per_launch_raw=(f + w) if f is not None and w is not None else None)
+    # the keys bench.py's --traffic-json reads (roofline.traffic of the dominant family)
+    res["family"] = kernel
+    res["hbm_bytes_per_launch"] = res["conv_hbm_bytes_per_launch"]
+    res["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py --steps 1 "
+                     "--warmup 0 --no-roofline; mean over every launch of the family; FETCH doubled "
+                     "(MI355X_MICROARCH.md HBM: gfx950 tallies 128-B reads at 64 B), WRITE as is; "
+                     "Infinity-Cache hits included")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
