@@ -21,9 +21,9 @@
 //    tile's input patch (+1 halo) and the chunk's weights (as duplicated pairs, read by broadcast
 //    ds_read_b128 straight into v_pk_fma_f32 operands) staged through LDS in 8-channel chunks.
 //
-// 3. conv1x1_smallcin_kernel — 1x1 convs with Cin <= 4 (g_a's first point conv and skip, 3 -> N):
-//    write-bound; one pixel per lane (four per lane with 16-byte stores where rows allow), Cout
-//    outputs from scalar weights.
+// 3. conv1x1_smallcin_kernel — 1x1 (and 3x3 pad 1) convs with Cin <= 4 (g_a's first point conv and
+//    skip, 3 -> N; the small-decoder model's dense first conv): write-bound; one pixel per lane (four
+//    per lane with 16-byte stores where rows allow), Cout outputs from scalar weights.
 #include "common.h"
 #include "kernels.h"
 
@@ -332,6 +332,8 @@ static int pw_mode(const ConvParams& P) {
   X(CIN, CT, 2, 0) X(CIN, CT, 2, 1) X(CIN, CT, 3, 0) X(CIN, CT, 3, 1)
 #define PW_COMBOS(X)                                                                              \
   PW_ALL(X, 96, 3) PW_ALL(X, 128, 4) PW_ALL(X, 160, 5) PW_ALL(X, 192, 6)                          \
+  /* MLICPP_M_SMALL_DEC's g_s (N / 4 = 48 channels at full resolution) */                         \
+  PW_ALL(X, 48, 2)                                                                                \
   /* LRP: 224 -> 128 GELU; head 128 -> 32 (0.5 tanh, checkerboard mask, residual into y_hat) */   \
   X(224, 4, 1, 0) X(128, 1, 4, 1)                                                                 \
   /* channel context (dwsep): 32i -> 192 GELU, 192 -> 128 GELU */                                 \
@@ -346,7 +348,8 @@ bool pw_resident_ok(const ConvParams& P, int cin_pad) {
   const int mode = pw_mode(P);
   if (mode < 0) return false;
   if (P.Ho != (P.H - 1) / P.stride + 1 || P.Wo != (P.W - 1) / P.stride + 1) return false;
-  if (P.seg[0].C != P.Cin || cin_pad != P.Cin) return false;
+  // the weight rows are read with stride cin_pad (>= Cin; padding columns are zeros)
+  if (P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.stride != 1 && (mode == 2 || mode == 3 || mode == 4)) return false;  // GDN aux is the conv input; mask grid
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
@@ -546,35 +549,49 @@ void conv_narrow_forward(const ConvParams& P, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// 1x1 conv (any stride, pad 0) with Cin <= 4: one output pixel per lane, exact fp32.
-template <int CIN>
+// KxK conv (K = 1 pad 0, or K = 3 pad 1; any stride) with Cin <= 4: one output pixel per lane, exact
+// fp32, taps outer and channels inner (the [tap][Cin][Cout] packing order); K = 3 serves
+// MLICPP_M_SMALL_DEC's dense first conv (3 -> N, stride 2)
+template <int CIN, int K>
+__device__ __forceinline__ float smallcin_in(const ConvParams& P, const float* xb, int64_t HWi, int c, int iy, int ix) {
+  if (K > 1 && (iy < 0 || iy >= P.H || ix < 0 || ix >= P.W)) return 0.0f;
+  float v = xb[c * HWi + (int64_t)iy * P.W + ix];
+  if (P.epi & EPI_SQUARE_IN) v *= v;
+  return v;
+}
+
+template <int CIN, int K>
 __global__ __launch_bounds__(256) void conv1x1_smallcin_kernel(ConvParams P) {
+  constexpr int KK = K * K;
   const int HWo = P.Ho * P.Wo;
   const int p = blockIdx.x * 256 + threadIdx.x;
   const int b = blockIdx.y;
   if (p >= HWo) return;
   const int oh = p / P.Wo, ow = p - oh * P.Wo;
   const int64_t HWi = (int64_t)P.H * P.W;
-  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs + (int64_t)(oh * P.stride) * P.W + ow * P.stride;
-  float xv[CIN];
+  const float* xb = P.seg[0].p + (int64_t)b * P.seg[0].bs;
+  float xv[KK][CIN];
 #pragma unroll
-  for (int c = 0; c < CIN; ++c) {
-    xv[c] = x[c * HWi];
-    if (P.epi & EPI_SQUARE_IN) xv[c] *= xv[c];
-  }
-  const float* w = P.wpk;  // [1][Cin][Cout]
+  for (int t = 0; t < KK; ++t)
+#pragma unroll
+    for (int c = 0; c < CIN; ++c)
+      xv[t][c] = smallcin_in<CIN, K>(P, xb, HWi, c, oh * P.stride + t / K - P.pad, ow * P.stride + t % K - P.pad);
+  const float* w = P.wpk;  // [K*K][Cin][Cout]
   for (int co = 0; co < P.Cout; ++co) {
     float v = 0.0f;
 #pragma unroll
-    for (int c = 0; c < CIN; ++c) v = fmaf(xv[c], w[c * P.Cout + co], v);
+    for (int t = 0; t < KK; ++t)
+#pragma unroll
+      for (int c = 0; c < CIN; ++c) v = fmaf(xv[t][c], w[(t * CIN + c) * P.Cout + co], v);
     conv_store(P, b, co, p, v);
   }
 }
 
 // the same with four consecutive output pixels of one row per lane and 16-byte stores (the layer is
 // write-bound: Cout = N outputs per input pixel); identical per-element arithmetic
-template <int CIN>
+template <int CIN, int K>
 __global__ __launch_bounds__(256) void conv1x1_smallcin_vec_kernel(ConvParams P) {
+  constexpr int KK = K * K;
   const int HWo = P.Ho * P.Wo;
   const int p = 4 * (blockIdx.x * 256 + threadIdx.x);
   const int b = blockIdx.y;
@@ -582,53 +599,61 @@ __global__ __launch_bounds__(256) void conv1x1_smallcin_vec_kernel(ConvParams P)
   const int oh = p / P.Wo, ow = p - oh * P.Wo;
   const int64_t HWi = (int64_t)P.H * P.W;
   const int S = P.stride;
-  const float* x = P.seg[0].p + (int64_t)b * P.seg[0].bs + (int64_t)(oh * S) * P.W + ow * S;
-  float xv[CIN][4];
+  const float* xb = P.seg[0].p + (int64_t)b * P.seg[0].bs;
+  float xv[KK][CIN][4];
 #pragma unroll
-  for (int c = 0; c < CIN; ++c)
+  for (int t = 0; t < KK; ++t)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      xv[c][e] = x[c * HWi + e * S];
-      if (P.epi & EPI_SQUARE_IN) xv[c][e] *= xv[c][e];
-    }
-  const float* w = P.wpk;  // [1][Cin][Cout]
+    for (int c = 0; c < CIN; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        xv[t][c][e] = smallcin_in<CIN, K>(P, xb, HWi, c, oh * S + t / K - P.pad, (ow + e) * S + t % K - P.pad);
+  const float* w = P.wpk;  // [K*K][Cin][Cout]
   for (int co = 0; co < P.Cout; ++co) {
     float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int c = 0; c < CIN; ++c) {
-      const float wc = w[c * P.Cout + co];
+    for (int t = 0; t < KK; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaf(xv[c][e], wc, v[e]);
-    }
+      for (int c = 0; c < CIN; ++c) {
+        const float wc = w[(t * CIN + c) * P.Cout + co];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(xv[t][c][e], wc, v[e]);
+      }
     conv_store4(P, b, co, p, make_float4(v[0], v[1], v[2], v[3]));
   }
 }
 
 bool conv_smallcin_ok(const ConvParams& P) {
-  return P.K == 1 && P.pad == 0 && P.nseg == 1 && P.Cin >= 1 && P.Cin <= 4;
+  return ((P.K == 1 && P.pad == 0) || (P.K == 3 && P.pad == 1)) && P.nseg == 1 && P.Cin >= 1 && P.Cin <= 4;
 }
 
-void conv_smallcin_forward(const ConvParams& P, hipStream_t st) {
-  MLIC_CHECK(conv_smallcin_ok(P), "conv_smallcin: unsupported shape");
+template <int K>
+static void launch_smallcin(const ConvParams& P, hipStream_t st) {
   if ((P.Wo & 3) == 0 && conv_vec_ok(P) && !(P.epi & EPI_SHUFFLE)) {
     dim3 grid((P.Ho * P.Wo / 4 + 255) / 256, P.B);
     switch (P.Cin) {
-      case 1: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<1>, grid, dim3(256), 0, st, P); break;
-      case 2: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<2>, grid, dim3(256), 0, st, P); break;
-      case 3: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<3>, grid, dim3(256), 0, st, P); break;
-      default: hipLaunchKernelGGL(conv1x1_smallcin_vec_kernel<4>, grid, dim3(256), 0, st, P); break;
+      case 1: hipLaunchKernelGGL((conv1x1_smallcin_vec_kernel<1, K>), grid, dim3(256), 0, st, P); break;
+      case 2: hipLaunchKernelGGL((conv1x1_smallcin_vec_kernel<2, K>), grid, dim3(256), 0, st, P); break;
+      case 3: hipLaunchKernelGGL((conv1x1_smallcin_vec_kernel<3, K>), grid, dim3(256), 0, st, P); break;
+      default: hipLaunchKernelGGL((conv1x1_smallcin_vec_kernel<4, K>), grid, dim3(256), 0, st, P); break;
     }
     HIP_OK(hipGetLastError());
     return;
   }
   dim3 grid((P.Ho * P.Wo + 255) / 256, P.B);
   switch (P.Cin) {
-    case 1: hipLaunchKernelGGL(conv1x1_smallcin_kernel<1>, grid, dim3(256), 0, st, P); break;
-    case 2: hipLaunchKernelGGL(conv1x1_smallcin_kernel<2>, grid, dim3(256), 0, st, P); break;
-    case 3: hipLaunchKernelGGL(conv1x1_smallcin_kernel<3>, grid, dim3(256), 0, st, P); break;
-    default: hipLaunchKernelGGL(conv1x1_smallcin_kernel<4>, grid, dim3(256), 0, st, P); break;
+    case 1: hipLaunchKernelGGL((conv1x1_smallcin_kernel<1, K>), grid, dim3(256), 0, st, P); break;
+    case 2: hipLaunchKernelGGL((conv1x1_smallcin_kernel<2, K>), grid, dim3(256), 0, st, P); break;
+    case 3: hipLaunchKernelGGL((conv1x1_smallcin_kernel<3, K>), grid, dim3(256), 0, st, P); break;
+    default: hipLaunchKernelGGL((conv1x1_smallcin_kernel<4, K>), grid, dim3(256), 0, st, P); break;
   }
   HIP_OK(hipGetLastError());
+}
+
+void conv_smallcin_forward(const ConvParams& P, hipStream_t st) {
+  MLIC_CHECK(conv_smallcin_ok(P), "conv_smallcin: unsupported shape");
+  if (P.K == 1) launch_smallcin<1>(P, st);
+  else launch_smallcin<3>(P, st);
 }
 
 }  // namespace mlic

@@ -69,7 +69,7 @@ def check(y, ref, rtol=2e-5):
     assert err <= rtol * scale + 1e-6, f"max err {err:.3e} (scale {scale:.3e})"
 
 
-@pytest.mark.parametrize("cin", [96, 128, 160, 192])
+@pytest.mark.parametrize("cin", [48, 96, 128, 160, 192])
 def test_pw_resident_sizes(cin):
     check(*run(PW, 2, cin, cin, 48, 80, 1))
 
@@ -77,6 +77,7 @@ def test_pw_resident_sizes(cin):
 @pytest.mark.parametrize("epi", [0, GELU, GDN | SQUARE, IGDN | SQUARE, GELU | RES, GDN | SQUARE | RES])
 def test_pw_resident_epilogues(epi):
     check(*run(PW, 2, 192, 192, 36, 60, 1, epi=epi))
+    check(*run(PW, 1, 48, 48, 37, 53, 1, epi=epi))  # small-decoder width: 3 k-steps, partial co-tile
 
 
 def test_pw_resident_stride2():
@@ -113,6 +114,9 @@ def test_smallcin(stride):
     check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride))               # 4-pixel vector path
     check(*run(SMALLCIN, 2, 3, 192, 64, 96, 1, stride=stride, epi=GELU | RES))
     check(*run(SMALLCIN, 1, 3, 192, 37, 53, 1, stride=stride, epi=GELU))      # odd width: scalar path
+    # 3x3 pad 1 (MLICPP_M_SMALL_DEC's dense first conv, 3 -> N stride 2): borders, both paths
+    check(*run(SMALLCIN, 2, 3, 192, 64, 96, 3, stride=stride, epi=GELU))
+    check(*run(SMALLCIN, 1, 3, 96, 37, 53, 3, stride=stride))
 
 
 @pytest.mark.parametrize("impl", [F32, X3, X3V2])
