@@ -82,9 +82,12 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int pad = K / 2;  // H, W: the tiling grid (= P.H, P.W, or H*W folded into rows of 32 for K = 1)
+  const int pad = K / 2;  // H, W: the tiling grid (= P.Ho, P.Wo, or H*W folded into rows of 32 for K = 1)
   const int npix = P.Ho * P.Wo;
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  // the packed input plane (zero border pad) and the stride: output (oy, ox), tap (ky, kx) reads the
+  // packed line (S oy + ky, S ox + kx)
+  const int S = K == 1 ? 1 : P.stride;
+  const int Hp = (K == 1 ? H : P.H) + 2 * pad, Wp = (K == 1 ? W : P.W) + 2 * pad;
   const int ntx = (W + TC - 1) / TC;
   const int nct = gridDim.x, npt = gridDim.y, nblk = nct * npt;
   const int bid = blockIdx.y * nct + blockIdx.x;
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     const int n = (wave * NB + i) * 8 + (lane >> 3);
     const int oy = min(oy0 + n / TC, H - 1), ox = min(ox0 + n % TC, W - 1);
     const int G = (lane & 7) ^ swz(n);
-    bsrc[i] = act + (int64_t)b * nchunk * plane + ((int64_t)oy * Wp + ox) * ROWH + G * 8;
+    bsrc[i] = act + (int64_t)b * nchunk * plane + ((int64_t)oy * S * Wp + ox * S) * ROWH + G * 8;
   }
   const _Float16* asrc = wx + ((int64_t)ct * nsteps * BM) * ROWH + (wave * NA) * 512 + lane * 8;
 
@@ -460,9 +463,13 @@ void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, i
 }
 // K = 1: no spatial coupling, so the flat pixel index is folded into rows of TC = 32: every
 // 8 x 32 tile is 256 consecutive pixels and only the image's last tile is ragged
-static void x4_grid(const ConvParams& P, int& H, int& W) {
+static void x4_grid(const ConvParams& P, int& H, int& W) {  // the packed input's grid
   H = P.K == 1 ? (P.H * P.W + TC - 1) / TC : P.H;
   W = P.K == 1 ? TC : P.W;
+}
+static void x4_tgrid(const ConvParams& P, int& H, int& W) {  // the output tiling grid
+  H = P.K == 1 ? (P.H * P.W + TC - 1) / TC : P.Ho;
+  W = P.K == 1 ? TC : P.Wo;
 }
 
 int64_t x4_act_halves(const ConvParams& P, int cin_pad, bool hi) {
@@ -473,8 +480,11 @@ int64_t x4_act_halves(const ConvParams& P, int cin_pad, bool hi) {
 }
 
 bool conv_x4_ok(const ConvParams& P, int cin_pad) {
-  if (!(P.K == 1 || P.K == 3 || P.K == 5) || P.stride != 1 || P.pad != P.K / 2) return false;
-  if (P.Ho != P.H || P.Wo != P.W || cin_pad % 32 != 0 || cin_pad < P.Cin || P.Cout < 32) return false;
+  // stride 1 (K = 1, 3, 5), or stride 2 for K = 3 (the small-decoder model's dense strided convs)
+  if (!(P.K == 1 || P.K == 3 || P.K == 5) || P.pad != P.K / 2) return false;
+  if (!(P.stride == 1 || (P.stride == 2 && P.K == 3))) return false;
+  if (P.Ho != (P.H - 1) / P.stride + 1 || P.Wo != (P.W - 1) / P.stride + 1) return false;
+  if (cin_pad % 32 != 0 || cin_pad < P.Cin || P.Cout < 32) return false;
   for (int s = 0; s + 1 < P.nseg; ++s)
     if (P.seg[s].C % 16 != 0) return false;
   return true;
@@ -526,7 +536,7 @@ template <int K, int BM>
 static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st,
                       int nsplit, bool hi) {
   int H, W;
-  x4_grid(P, H, W);
+  x4_tgrid(P, H, W);
   const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
   dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B * nsplit);
   static const int abl = [] {
@@ -555,7 +565,7 @@ int x4_splitk(const ConvParams& P, int cin_pad, bool hi) {
   }();
   if (!on || !x4_rs() || P.K == 1) return 1;
   int H, W;
-  x4_grid(P, H, W);
+  x4_tgrid(P, H, W);
   const int tiles = ((P.Cout + x4_bm(P.Cout) - 1) / x4_bm(P.Cout)) * ((W + TC - 1) / TC) * ((H + TR - 1) / TR);
   const int nsteps = x4_nchunk(cin_pad, hi) * P.K * P.K;
   if (tiles > 48 || nsteps < 48) return 1;

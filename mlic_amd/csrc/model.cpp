@@ -305,9 +305,11 @@ void Model::add_chains(hipStream_t st) {
       else if (w.Cin != c.cout[l - 1]) ok = false;
       total += chain_layer_halves(w.Cout, w.Cin);
     }
-    if (ok && chain_supported(c.nl, c.cout) && c.cin0 % 64 == 0) {  // even K-step count (chain.hip)
-      cws.push_back(c);
-      if (c.nl == 4 && c.cin0 >= hyp && (c.cin0 - hyp) % 64 == 0) {  // the hoisted variant: context columns
+    if (ok && chain_supported(c.nl, c.cout)) {
+      if (c.cin0 % 64 == 0) cws.push_back(c);  // even K-step count (chain.hip)
+      // the hoisted variant (context columns only) also serves EPs whose full input is an odd number of
+      // 32-channel chunks (MLICPP_M_SMALL_DEC: 2 hM = 160 hyper channels)
+      if (c.nl == 4 && c.cin0 >= hyp && (c.cin0 - hyp) % 64 == 0) {
         ChainW h = c;
         h.cin0 = c.cin0 - hyp;
         h.name = c.name + "#ctx";

@@ -179,6 +179,16 @@ def test_x4(shape):
     check(*run(X4, B, cin, cout, H, W, K, epi=epi))
 
 
+@pytest.mark.parametrize("shape", [
+    (2, 192, 192, 34, 60, 0),      # small-decoder g_a / h_a stride-2 dense conv
+    (1, 192, 192, 33, 47, 1),      # odd input: the last output row / column reads the zero border
+    (1, 320, 192, 17, 30, 1),      # 10 chunks, small grid: the split-K path
+])
+def test_x4_stride2(shape):
+    B, cin, cout, H, W, epi = shape
+    check(*run(X4, B, cin, cout, H, W, 3, stride=2, epi=epi))
+
+
 def _fp16_operands(x, w):
     """The operands the reduced-precision x4 form multiplies: x rounded to fp16, w rounded to fp16
     after the layer's exact power-of-two prescale (max |w| * 2^e in [2^14, 2^15), split_weights)."""
