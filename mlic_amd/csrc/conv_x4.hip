@@ -369,9 +369,8 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   const int pos = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   const int cc = blockIdx.y, b = blockIdx.z;
-  if (pos >= Hp * Wp) return;
   const int y = pos / Wp - Q.pad, x = pos % Wp - Q.pad;
-  const bool inb = y >= 0 && y < Q.H && x >= 0 && x < Q.W && y * Q.W + x < Q.npix;
+  const bool inb = pos < Hp * Wp && y >= 0 && y < Q.H && x >= 0 && x < Q.W && y * Q.W + x < Q.npix;
   const int64_t HW = Q.npix;  // channel plane stride of the (unfolded) input
   bool bad = false;
   // 8 consecutive channels from ch0 (8-channel groups never straddle a segment: segments are
@@ -407,9 +406,23 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
       l[j] = (_Float16)(v[j] - (float)hv);
     }
   }
-  _Float16* d = Q.dst + (((int64_t)b * Q.nchunk + cc) * Hp * Wp + pos) * ROWH + 8 * g;
-  *reinterpret_cast<half8*>(d) = h;
-  *reinterpret_cast<half8*>(d + 32) = l;
+  // the block's 64 lines are 8 KB contiguous in the destination: assemble them in LDS (rows padded
+  // to 144 B: conflict-free 16-byte writes) and store them lane-consecutively, whole lines per
+  // instruction (a direct store would scatter 16-byte pieces over 64 lines per instruction)
+  constexpr int SP = ROWH + 8;
+  __shared__ __attribute__((aligned(16))) _Float16 stg[64 * SP];
+  const int lane = threadIdx.x & 63;
+  *reinterpret_cast<half8*>(stg + lane * SP + 8 * g) = h;
+  *reinterpret_cast<half8*>(stg + lane * SP + 32 + 8 * g) = l;
+  __syncthreads();
+  const int nlines = min(64, Hp * Wp - (int)blockIdx.x * 64);
+  _Float16* d = Q.dst + (((int64_t)b * Q.nchunk + cc) * Hp * Wp + (int64_t)blockIdx.x * 64) * ROWH;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = k * 256 + threadIdx.x;  // 16-byte piece: line q / 8, granule q % 8
+    if (q / 8 < nlines)
+      *reinterpret_cast<half8*>(d + q * 8) = *reinterpret_cast<const half8*>(stg + (q / 8) * SP + (q % 8) * 8);
+  }
   range_report(Q.rflag, bad);
 }
 
