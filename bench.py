@@ -512,6 +512,16 @@ def profile_roofline(a, nets, groups, xs, is_vbr, t_step_s, dev):
                 # against the measured step time
                 "step_t_roof_ms": round(t_roof, 3), "step_ms": round(1e3 * t_step_s, 3),
                 "step_frac": round(t_roof / max(1e-9, 1e3 * t_step_s), 4)}
+    # the runner-up families too (the top two are often within a few % of each other: the choice
+    # between them is not stable across boxes, and rocprofv3 may rank them the other way)
+    others = []
+    for k in sorted(fam, key=lambda k: -fam[k]["ms"])[1:3]:
+        b_, u_, a_, p_, _ = bound_of(fam[k], k)
+        others.append({"kernel": k, "bound": b_, "achieved": round(a_, 3), "peak": round(p_, 1), "unit": u_,
+                       "frac": round(a_ / p_, 4), "launches_per_step": fam[k]["launches"],
+                       "avg_launch_us": round(1000 * fam[k]["ms"] / max(1, fam[k]["launches"]), 2),
+                       "share_of_gpu_time": round(fam[k]["ms"] / max(1e-9, sum(v["ms"] for v in fam.values())), 4)})
+    roofline["runners_up"] = others
     if iso:
         _, _, ach1, _, _ = bound_of(iso, dom)
         roofline["isolated"] = {"achieved": round(ach1, 3), "frac": round(ach1 / peak, 4), "images": share,

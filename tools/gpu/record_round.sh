@@ -24,6 +24,12 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   python3 -u bench.py --no-cpu-baseline --traffic-json "$OUT/traffic.json" > "$OUT/bench_under_rocprof.json" \
   2> "$OUT/rocprof.err" || { echo "rocprof stats failed $?"; tail -20 "$OUT/rocprof.err"; exit 1; }
 rm -f "$OUT"/prof/run_kernel_trace.csv
+# the timed workload alone (no profiled passes): its per-launch averages are the ones the line's
+# roofline divides by (the run above also holds the one-lane isolated pass, whose launches are shorter)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_timed" -o run -- \
+  python3 -u bench.py --no-cpu-baseline --no-roofline > "$OUT/bench_under_rocprof_timed.json" \
+  2> "$OUT/rocprof_timed.err" || { echo "rocprof timed stats failed $?"; tail -20 "$OUT/rocprof_timed.err"; exit 1; }
+rm -f "$OUT"/prof_timed/run_kernel_trace.csv
 timeout -k 10 400 python3 -u bench.py --synth-fp16 --no-cpu-baseline --traffic-json "$OUT/traffic.json" \
   --layers-out "$OUT/layers_synth_fp16.tsv" > "$OUT/bench_synth_fp16.json" 2> "$OUT/bench_synth_fp16.err" ||
   { echo "bench synth-fp16 failed $?"; tail -20 "$OUT/bench_synth_fp16.err"; exit 1; }
