@@ -121,3 +121,30 @@ def test_pmf_to_quantized_cdf_properties():
         c = entropy.pmf_to_quantized_cdf(p)
         assert c[0] == 0 and c[-1] == 1 << 16
         assert np.all(np.diff(c) >= 1)
+
+
+def test_conv_choice_pins_the_measured_selection():
+    """The kernel family per layer shape that round 2's A/B measurements chose; a
+    regression here changes speed (and, as families round differently, the exact bits)."""
+    F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, X4 = range(8)
+    impl = C.c_int()
+
+    def choice(Cin, Cout, H, W, K, stride=1, B=8, epi=0):
+        _lib.call("mlic_conv_choice", B, Cin, Cout, H, W, K, stride, epi, C.byref(impl))
+        return impl.value
+
+    assert choice(192, 768, 272, 480, 3) == X4            # g_s subpel convs
+    assert choice(320, 1280, 8, 12, 3) == X4              # h_s subpel at the Kodak z grid (split-K)
+    assert choice(192, 192, 544, 960, 1) == PW            # full-resolution point convs
+    assert choice(224, 128, 32, 48, 1, epi=1) == PW       # Kodak-size LRP.2 (GELU): resident from 1 K px
+    assert choice(224, 128, 17, 30, 1, epi=1) != PW       # below 1 K px/image
+    assert choice(288, 288, 68, 120, 1) == X4             # context q/k/v (Cin <= 352)
+    assert choice(640, 224, 68, 120, 1) == X3V2           # 1080p LRP: x3v2 1.1x faster
+    assert choice(640, 224, 32, 48, 1) == X4              # Kodak LRP: small grid, x4 1.3x
+    assert choice(640, 6400, 68, 120, 1) == X4            # hoisted EntropyParameters GEMM
+    assert choice(288, 96, 68, 120, 5) == X4              # 5x5 reprojections
+    assert choice(192, 192, 544, 960, 3, stride=2) == X4  # small-decoder dense strided conv
+    assert choice(3, 192, 1088, 1920, 3, stride=2) == SMALLCIN
+    assert choice(3, 192, 1088, 1920, 1, stride=2) == SMALLCIN
+    assert choice(192, 12, 544, 960, 3) == NARROW
+    assert choice(48, 48, 1088, 1920, 1) == PW            # small-decoder g_s width
