@@ -42,20 +42,14 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   if ((int64_t)P.Ho * P.Wo >= 1024 && pw_resident_ok(P, w.cin_pad)) return CONV_PW;
   // x4: the dense 3x3 convs with wide Cout (g_s / h_s subpel convs), the 5x5 reprojections, the big
   // 1x1 GEMMs (the hoisted EntropyParameters hyper columns, h_s's last layer: Cin x Cout >= 2^18) and
-  // the mid-size 1x1s with Cin, Cout >= 192 that the resident kernel does not serve.  3x3 and 5x5 take
-  // any grid: the split-K path (x4_splitk) fills the chip for few-tile shapes (h_s at the z grid,
-  // 8 x 12 .. 17 x 30: 1.5-2.5x x3v2).  Mid-size 1x1s: x4 on small grids (< 32 tiles per image, e.g.
-  // the Kodak-size latent: 1.3-2.1x x3v2) and for Cin <= 352 (context q/k/v 224..288, the LRP of slice
-  // 0: 1.1-1.3x); the LRP's wider 384..640 -> 224 at the 1080p latent stay on x3v2 (1.1x faster there)
+  // the mid-size 1x1s with Cin, Cout >= 192 that the resident kernel does not serve (context q/k/v
+  // 224..288, the LRP's 352..640 -> 224, the small-decoder EntropyParameters: 1.07-2.1x x3v2 on the
+  // 1080p and Kodak-size latents, the activation pack included).  Any grid: the split-K path
+  // (x4_splitk) fills the chip for few-tile 3x3 / 5x5 shapes (h_s at the z grid, 8 x 12 .. 17 x 30:
+  // 1.5-2.5x x3v2)
   const bool big1 = (int64_t)P.Cin * P.Cout >= (1 << 18), mid1 = P.Cin >= 192 && P.Cout >= 192;
   const bool x4_shape = P.K == 1 ? (big1 || mid1) : P.Cout >= (P.K == 3 ? 192 : 64);
-  if (w.wx4 && x4_on() && x4_k_on(P.K) && x4_shape && conv_x4_ok(P, w.cin_pad)) {
-    if (P.K != 1) return CONV_X4;
-    const int bm = x4_bm(P.Cout);
-    const int64_t rows = ((int64_t)P.H * P.W + 31) / 32;
-    const bool small_grid = (int64_t)((P.Cout + bm - 1) / bm) * ((rows + 7) / 8) < 32;
-    if (small_grid || big1 || P.Cin <= 352) return CONV_X4;
-  }
+  if (w.wx4 && x4_on() && x4_k_on(P.K) && x4_shape && conv_x4_ok(P, w.cin_pad)) return CONV_X4;
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay
   if (P.K == 5 && conv_halo_ok(P, w.cin_pad) &&

@@ -139,8 +139,9 @@ def test_conv_choice_pins_the_measured_selection():
     assert choice(224, 128, 32, 48, 1, epi=1) == PW       # Kodak-size LRP.2 (GELU): resident from 1 K px
     assert choice(224, 128, 17, 30, 1, epi=1) != PW       # below 1 K px/image
     assert choice(288, 288, 68, 120, 1) == X4             # context q/k/v (Cin <= 352)
-    assert choice(640, 224, 68, 120, 1) == X3V2           # 1080p LRP: x3v2 1.1x faster
-    assert choice(640, 224, 32, 48, 1) == X4              # Kodak LRP: small grid, x4 1.3x
+    assert choice(640, 224, 68, 120, 1, epi=1) == X4      # 1080p LRP point conv: 1.07x x3v2
+    assert choice(640, 224, 32, 48, 1, epi=1) == X4       # Kodak LRP: 1.3x
+    assert choice(160, 96, 68, 120, 1) == X3V2            # narrow latent 1x1s without a resident form
     assert choice(640, 6400, 68, 120, 1) == X4            # hoisted EntropyParameters GEMM
     assert choice(288, 96, 68, 120, 5) == X4              # 5x5 reprojections
     assert choice(192, 192, 544, 960, 3, stride=2) == X4  # small-decoder dense strided conv
