@@ -236,9 +236,11 @@ def test_1080p_parity_and_roundtrip():
     assert 8 * nbytes / (H * W) <= bg * 1.01 + 0.01
 
 
-def test_kodak_size_parity():
-    """BASELINE config 1 shape (768x512) and its portrait twin, vs the CPU oracle."""
-    name = "MLICPP_L"
+@pytest.mark.parametrize("name", ["MLICPP_L", "MLICPP_S", "MLICPP_M_SMALL_DEC"])
+def test_kodak_size_parity(name):
+    """BASELINE config 1 shape (768x512) and its portrait twin, vs the CPU oracle: at this size the
+    latent grid is 32 x 48 (the resident 1x1 kernel, x4's small-grid and split-K paths) and, for the
+    small-decoder model, the dense stride-2 convs run on x4."""
     sd = synthetic.synth_state_dict(name, 0)
     m = ref.RefMLIC(name, sd)
     for H, W in ((512, 768), (768, 512)):
@@ -247,8 +249,12 @@ def test_kodak_size_parity():
         out = net_for(name)(x.to(DEV))
         torch.cuda.synchronize()
         bc = ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"], o["likelihoods"]["z_likelihoods"], H * W)
-        assert abs(bpp(out, H * W) - bc) <= 1e-3
-        assert abs(ref.psnr_uint8(x, out["x_hat"].cpu()) - ref.psnr_uint8(x, o["x_hat"])) <= 0.01
+        bg = bpp(out, H * W)
+        pg, pc = ref.psnr_uint8(x, out["x_hat"].cpu()), ref.psnr_uint8(x, o["x_hat"])
+        PARITY[f"kodak_{name}_{H}x{W}"] = {"bpp_gpu": bg, "bpp_cpu": bc, "psnr_gpu": pg, "psnr_cpu": pc,
+                                            "xhat_psnr_vs_cpu_db": _psnr_f(out["x_hat"].cpu(), o["x_hat"])}
+        assert abs(bg - bc) <= 1e-3, PARITY[f"kodak_{name}_{H}x{W}"]
+        assert abs(pg - pc) <= 0.01, PARITY[f"kodak_{name}_{H}x{W}"]
 
 
 def test_file_format_roundtrip(tmp_path):
