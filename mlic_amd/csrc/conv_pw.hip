@@ -334,6 +334,8 @@ static int pw_mode(const ConvParams& P) {
   PW_ALL(X, 96, 3) PW_ALL(X, 128, 4) PW_ALL(X, 160, 5) PW_ALL(X, 192, 6)                          \
   /* MLICPP_M_SMALL_DEC's g_s (N / 4 = 48 channels at full resolution) */                         \
   PW_ALL(X, 48, 2)                                                                                \
+  /* g_s's output conv as per-tap partials: N -> 9 x 12 = 108 rows */                             \
+  X(192, 4, 0, 0) X(96, 4, 0, 0) X(48, 4, 0, 0)                                                   \
   /* LRP: 224 -> 128 GELU; head 128 -> 32 (0.5 tanh, checkerboard mask, residual into y_hat) */   \
   X(224, 4, 1, 0) X(128, 1, 4, 1)                                                                 \
   /* channel context (dwsep): 32i -> 192 GELU, 192 -> 128 GELU */                                 \
@@ -545,6 +547,51 @@ void conv_narrow_forward(const ConvParams& P, hipStream_t st) {
   MLIC_CHECK(conv_narrow_ok(P), "conv_narrow: unsupported shape");
   dim3 grid((P.Wo + NR_TW - 1) / NR_TW, (P.Ho + NR_TH - 1) / NR_TH, P.B);
   hipLaunchKernelGGL(conv3x3_narrow_kernel<12>, grid, dim3(256), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// The N -> 12 3x3 output conv of g_s as a 1x1 conv N -> 9 x 12 (per-tap partial products, on the
+// resident MFMA kernel) plus this gather: out = bias + sum over the 9 taps (fixed order) of the
+// shifted partials, written through the PixelShuffle(2) (channel c = 4 c' + 2 dy + dx) as float2 pairs
+// (dx = 0, 1).  part [B][9 * 12][H][W] (row tap * 12 + c), out [B][3][2H][2W].
+__global__ __launch_bounds__(256) void taps_gather_kernel(const float* __restrict__ part, int64_t part_bs,
+                                                          const float* __restrict__ bias, float* __restrict__ out,
+                                                          int64_t out_bs, int H, int W) {
+  constexpr int C = 12;
+  const int w = blockIdx.x * 64 + (threadIdx.x & 63), h = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
+  if (w >= W || h >= H) return;
+  const int64_t HW = (int64_t)H * W;
+  const float* pb = part + (int64_t)b * part_bs;
+  float acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int y = h + t / 3 - 1, x = w + t % 3 - 1;
+    if (y < 0 || y >= H || x < 0 || x >= W) continue;
+    const float* q = pb + (int64_t)t * C * HW + (int64_t)y * W + x;
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] += q[c * HW];
+  }
+  float* ob = out + (int64_t)b * out_bs;
+  const int W2 = 2 * W;
+  const int64_t HW4 = 4 * HW;
+#pragma unroll
+  for (int cq = 0; cq < 3; ++cq)
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const int c = 4 * cq + 2 * dy;
+      const float b0 = bias ? bias[c] : 0.0f, b1 = bias ? bias[c + 1] : 0.0f;
+      *reinterpret_cast<float2*>(ob + cq * HW4 + (int64_t)(2 * h + dy) * W2 + 2 * w) =
+          make_float2(acc[c] + b0, acc[c + 1] + b1);
+    }
+}
+
+void taps_gather(const float* part, int64_t part_bs, const float* bias, float* out, int64_t out_bs, int H, int W,
+                 int B, hipStream_t st) {
+  hipLaunchKernelGGL(taps_gather_kernel, dim3((W + 63) / 64, (H + 3) / 4, B), dim3(256), 0, st, part, part_bs, bias,
+                     out, out_bs, H, W);
   HIP_OK(hipGetLastError());
 }
 

@@ -29,6 +29,10 @@ bool conv_narrow_ok(const ConvParams& P);
 void conv_narrow_forward(const ConvParams& P, hipStream_t st);
 bool conv_halo_ok(const ConvParams& P, int cin_pad);
 void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
+// g_s's N -> 12 3x3 output conv as 1x1 per-tap partials [B][108][H][W] + this gather (conv_pw.hip):
+// out [B][3][2H][2W] = PixelShuffle(2)(bias + sum over taps of the shifted partials)
+void taps_gather(const float* part, int64_t part_bs, const float* bias, float* out, int64_t out_bs, int H, int W,
+                 int B, hipStream_t st);
 bool conv_smallcin_ok(const ConvParams& P);
 void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 

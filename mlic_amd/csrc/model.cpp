@@ -135,6 +135,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
       pack_conv(ptrs[i], dst, w.Cout, w.Cin, w.K * w.K, st);
       if (k.find("local_context") != std::string::npos && ends_with(k, ".fusion.weight") && w.Cin == 800)
         add_fusion_x4(base, ptrs[i], w.Cout, st);
+      if (base == "g_s.synthesis_transform.7.0" && w.K == 3 && w.Cout == 12) add_taps(base, ptrs[i], w.Cin, st);
       if (w.Cin >= 16) {  // split-fp16 copy for the f16x3 MFMA path
         w.cin_pad = (w.Cin + 31) / 32 * 32;
         const int64_t nh = (int64_t)w.Cout * w.K * w.K * w.cin_pad;
@@ -270,6 +271,33 @@ void Model::add_fusion_x4(const std::string& base, const float* w_dev, int Cout,
   cw.wexp = wexp;
   cw.name = base;
   convs_[base + ".__x4perm"] = cw;
+}
+
+// g_s's output conv (subpel_conv3x3(N, 3, 2): N -> 12, 3x3) as a 1x1 conv N -> 9 x 12 whose row
+// tap * 12 + c holds w[c][:][tap]: the per-tap partial products, summed by taps_gather
+void Model::add_taps(const std::string& base, const float* w_dev, int Cin, hipStream_t st) {
+  constexpr int C = 12;
+  std::vector<float> w((size_t)C * Cin * 9), wt((size_t)9 * C * Cin);
+  HIP_OK(hipMemcpyAsync(w.data(), w_dev, w.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  for (int c = 0; c < C; ++c)
+    for (int ci = 0; ci < Cin; ++ci)
+      for (int t = 0; t < 9; ++t) wt[((size_t)t * C + c) * Cin + ci] = w[((size_t)c * Cin + ci) * 9 + t];
+  float* tmp = nullptr;
+  HIP_OK(hipMalloc(&tmp, wt.size() * 4));
+  HIP_OK(hipMemcpyAsync(tmp, wt.data(), wt.size() * 4, hipMemcpyHostToDevice, st));
+  convs_[base + ".__taps"] = make_conv(tmp, 9 * C, Cin, 1, base + ".__taps", st);
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipFree(tmp));
+}
+
+// $MLIC_TAPS=0: g_s's output conv on the narrow VALU kernel (A/B switch)
+bool Model::taps_on() const {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_TAPS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && precision_ == PREC_F16X3_V2;
 }
 
 // LDS weight images of the fused chains: EntropyParameters (entropy.py:10-18, layers .0 .2 .4 .6) and
@@ -842,7 +870,21 @@ void Model::g_s(const View& yh, const View& out) {
   View e = rb(d, g + ".4", true);
   View f = rbu(e, g + ".5");
   View h = rb(f, g + ".6", true);
-  conv({h}, cw(g + ".7.0"), 1, 1, out, EPI_SHUFFLE);
+  auto tp = convs_.find(g + ".7.0.__taps");
+  const ConvW& w7 = cw(g + ".7.0");
+  if (tp != convs_.end() && taps_on()) {
+    // per-tap partials on the resident 1x1 kernel, then the fixed-order tap sum + bias + shuffle
+    const size_t m2 = L().arena.mark();
+    View part = alloc(tp->second.Cout, h.H, h.W);
+    conv({h}, tp->second, 1, 0, part, EPI_NONE);
+    const double pix = (double)L().B * h.H * h.W;
+    timed(PCAT_CONV_NARROW, pix * 9 * 12, 4.0 * pix * (9 * 12 + 12), [&] {
+      taps_gather(part.p, part.bs, w7.b, out.p, out.bs, h.H, h.W, L().B, L().st);
+    }, g + ".7.0.__gather");
+    L().arena.release(m2);
+  } else {
+    conv({h}, w7, 1, 1, out, EPI_SHUFFLE);
+  }
   L().arena.release(m);
 }
 

@@ -233,6 +233,8 @@ class Model {
                          const View* aux, const View* res);
   void run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi = false);
   void add_fusion_x4(const std::string& base, const float* w_dev, int Cout, hipStream_t st);
+  void add_taps(const std::string& base, const float* w_dev, int Cin, hipStream_t st);
+  bool taps_on() const;
   void conv_pair(const std::vector<View>& ins, const ConvW& w1, const View& out1, int epi1, const ConvW& w2,
                  const View& out2, int epi2);
   void dw(const std::vector<View>& ins, const DwW& w, int stride, const View& out, bool gelu);
