@@ -239,7 +239,7 @@ def main():
     if "MLIC_HOST_THREADS" not in os.environ:
         os.environ["MLIC_HOST_THREADS"] = str(max(2, min(16, len(cores))))
 
-    from mlic_amd import _lib, get_model, synthetic
+    from mlic_amd import _lib, bitstream, get_model, synthetic
     from mlic_amd import dist as mdist
     wl = WORKLOADS[a.config]
     jobs, n_jobs_total = build_jobs(a, rank, world)
@@ -320,7 +320,8 @@ def main():
             kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
             c = net.compress(xs[gi], **kw)
         for i, j in enumerate(js):
-            nbytes = len(c["strings"][0][i]) + len(c["strings"][1][i])
+            # the file the harness writes (header included, utils/utils.py:71-83), as bitstream.write_stream
+            nbytes = bitstream.file_bytes(len(c["strings"][0][i]), len(c["strings"][1][i]), vbr=is_vbr)
             yb, zb = net.likelihood_bits(i)
             rec[r, F["job"]] = j.id
             rec[r, F["H"]], rec[r, F["W"]] = H, W

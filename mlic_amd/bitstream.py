@@ -21,6 +21,12 @@ import torch
 import torch.nn.functional as F
 
 
+def file_bytes(y_len: int, z_len: int, vbr: bool = False) -> int:
+    """Size of the file write_stream produces for one image's y and z streams (the header included:
+    bpp_file = 8 * file_bytes / (H * W), utils/utils.py:71-83)."""
+    return (12 if vbr else 8) + 12 + (4 + y_len) + (4 + z_len)
+
+
 def write_stream(fd, H: int, W: int, shape, strings, level=None) -> int:
     n = 0
     if level is None:

@@ -359,10 +359,12 @@ int mlic_conv_choice(int B, int Cin, int Cout, int H, int W, int K, int stride, 
     P.B = B;
     P.epi = epi;
     const int cin_pad = (Cin + 31) / 32 * 32;
-    // weight pointers only signal presence (the model holds split and x4 images for these layers)
+    // weight pointers only signal presence, by the model's own allocation rule (model.cpp: split
+    // fp16 copies for Cin >= 16, x4 images of those for K in {1, 3, 5} and Cout >= 64)
     static const _Float16 tag = 0;
-    const bool x4 = Cout >= 64;
-    const ConvWeights cw{nullptr, &tag, &tag, cin_pad, x4 ? &tag : nullptr, 0};
+    const bool split = Cin >= 16;
+    const bool x4 = split && Cout >= 64;
+    const ConvWeights cw{nullptr, split ? &tag : nullptr, split ? &tag : nullptr, cin_pad, x4 ? &tag : nullptr, 0};
     *impl = conv_select(P, cw, 2);
   });
 }

@@ -86,9 +86,6 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
   HIP_OK(hipMalloc(&block, total));
   owned_.push_back(block);
   wbytes_ = total;
-  HIP_OK(hipMalloc(&rflag_, sizeof(int)));
-  owned_.push_back(rflag_);
-  HIP_OK(hipMemsetAsync(rflag_, 0, sizeof(int), st));
   size_t off = 0;
   auto take = [&](int64_t nf) {
     char* p = block + off;
@@ -297,7 +294,7 @@ bool Model::taps_on() const {
     const char* e = std::getenv("MLIC_TAPS");
     return !(e && std::atoi(e) == 0);
   }();
-  return on && precision_ == PREC_F16X3_V2;
+  return on && prec() == PREC_F16X3_V2;
 }
 
 // LDS weight images of the fused chains: EntropyParameters (entropy.py:10-18, layers .0 .2 .4 .6) and
@@ -445,7 +442,7 @@ bool Model::dwpw_on() const {
     const char* e = std::getenv("MLIC_DWPW");
     return e && std::atoi(e) == 1;
   }();
-  return on && precision_ == PREC_F16X3_V2;
+  return on && prec() == PREC_F16X3_V2;
 }
 
 // $MLIC_CHAIN=0: the per-layer path for EntropyParameters / LocalContext MLP (A/B switch)
@@ -454,7 +451,7 @@ bool Model::chain_on() const {
     const char* e = std::getenv("MLIC_CHAIN");
     return !(e && std::atoi(e) == 0);
   }();
-  return on && precision_ == PREC_F16X3_V2;
+  return on && prec() == PREC_F16X3_V2;
 }
 
 Model::~Model() {
@@ -463,6 +460,7 @@ Model::~Model() {
 }
 
 Lane::~Lane() {
+  if (rflag) (void)hipFree(rflag);
   if (h_sym) (void)hipHostFree(h_sym);
   if (h_idx) (void)hipHostFree(h_idx);
   for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
@@ -489,6 +487,8 @@ Lane& Model::lane(int i) {
     }
     l->own_stream = true;
     l->prof = prof_;
+    HIP_OK(hipMalloc(&l->rflag, sizeof(int)));
+    HIP_OK(hipMemsetAsync(l->rflag, 0, sizeof(int), l->st));
     lanes_.push_back(std::move(l));
   }
   return *lanes_[i];
@@ -550,7 +550,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
   const ConvParams P1 = conv_params(ins, w1, 1, w1.K / 2, out1, epi1, nullptr, nullptr);
   const ConvParams P2 = conv_params(ins, w2, 1, w2.K / 2, out2, epi2, nullptr, nullptr);
   const ConvWeights c1{w1.w, w1.wh, w1.wl, w1.cin_pad, w1.wx4, w1.wexp}, c2{w2.w, w2.wh, w2.wl, w2.cin_pad, w2.wx4, w2.wexp};
-  if (conv_select(P1, c1, precision_) != CONV_X4 || conv_select(P2, c2, precision_) != CONV_X4 ||
+  if (conv_select(P1, c1, prec()) != CONV_X4 || conv_select(P2, c2, prec()) != CONV_X4 ||
       w1.cin_pad != w2.cin_pad || w1.K != w2.K) {
     run_conv(P1, w1, nullptr);
     run_conv(P2, w2, nullptr);
@@ -570,7 +570,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
 // packed: the input already in x4's split layout (conv_pair); the impl is then necessarily x4
 void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi) {
   const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4, w.wexp};
-  const int impl = packed ? (hi ? CONV_X4H : CONV_X4) : conv_select(P, cw, precision_);
+  const int impl = packed ? (hi ? CONV_X4H : CONV_X4) : conv_select(P, cw, prec());
   const double outn = (double)P.B * w.Cout * P.Ho * P.Wo;
   const double flops = 2.0 * outn * P.Cin * w.K * w.K;
   const double bytes = 4.0 * ((double)P.B * P.Cin * P.H * P.W + (double)w.Cout * P.Cin * w.K * w.K +
@@ -617,7 +617,7 @@ ConvParams Model::conv_params(const std::vector<View>& ins, const ConvW& w, int 
   P.Wo = (P.W + 2 * pad - w.K) / stride + 1;
   P.wpk = w.w;
   P.wexp = w.wexp;  // conv_run clears it for the fp32 families
-  P.rflag = rflag_;
+  P.rflag = L().rflag;
   P.bias = w.b;
   P.epi = epi;
   if (epi & EPI_SHUFFLE) {
@@ -700,7 +700,7 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
     P.wexp[l] = c.wexp[l];
   }
   P.wimg = c.wimg;
-  P.rflag = rflag_;
+  P.rflag = L().rflag;
   P.out = out.p;
   P.out_bs = out.bs;
   if (res) {
@@ -906,7 +906,7 @@ View Model::local_context(const View& x, int i) {
     const char* e = std::getenv("MLIC_LA_PACKED");
     return !(e && std::atoi(e) == 0);
   }();
-  if (packed_on && precision_ == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm")) {
+  if (packed_on && prec() == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm")) {
     // attention straight into the fusion conv's packed split operand, fusion on conv_x4
     const ConvW& fw = cw(p + ".fusion.__x4perm");
     const int npos = (H * W + 31) / 32 * 32;
@@ -1289,7 +1289,9 @@ void Model::set_vbr(const float* scales, int B) {
   if (!l.vbr_on) return;
   for (int b = 0; b < B; ++b) {
     const float s = scales ? scales[b] : 1.0f;
-    MLIC_CHECK(std::isfinite(s) && s > 0.0f, "VBR gain must be finite and positive");
+    // forward uses Gain[s] as stored (mlicpp_vbr.py:122-135); compress/decompress receive |Gain[s]|
+    // from the Python layer (mlicpp_vbr.py:543, 899)
+    MLIC_CHECK(std::isfinite(s) && s != 0.0f, "VBR gain must be finite and nonzero");
     l.vbr_host[b] = s;
     l.vbr_host[B + b] = 1.0f / s;  // mlicpp_vbr.py: rescale by 1 / scale
   }
@@ -1427,17 +1429,18 @@ void Model::over_lanes(int B, hipStream_t caller, F&& fn) {
 void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_lik, float* z_lik, const float* vbr_scales,
                     hipStream_t st) {
   MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64 (pad like utils/testing.py:130-137)");
-  // forward() runs on the caller's stream in lane 0 (torch-ordered, capturable)
+  // forward() runs on the caller's stream in lane 0 (torch-ordered)
   Lane& l = lane(0);
   hipStream_t own = l.st;
   tl_lane_ = &l;
   struct Restore {
     Lane& l;
     hipStream_t s;
-    ~Restore() { l.st = s; tl_lane_ = nullptr; }
+    ~Restore() { l.st = s; l.prec_force = -1; tl_lane_ = nullptr; }
   } restore{l, own};
   l.st = st;  // caller's stream, including the legacy NULL stream torch uses by default
   set_vbr(vbr_scales, B);
+  range_clear(l);
   auto body = [&] {
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
@@ -1453,37 +1456,36 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
     }
   };
   planned(B, st, body);
-  if (precision_ != PREC_F32 && range_hit(st)) {
+  // The fp16 range guard needs a device-to-host read, i.e. a synchronisation of `st`; under stream
+  // capture (hipGraph) there is none, and a captured forward cannot fall back: its flag stays set
+  // for the caller to read.  Otherwise forward() returns with `st` synchronised.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_OK(hipStreamIsCapturing(st, &cap));
+  if (cap == hipStreamCaptureStatusNone && prec() != PREC_F32 && range_hit(l)) {
     // an activation left fp16's range in a split-fp16 kernel: the whole call again in exact fp32 MFMA
-    const int keep = precision_;
-    precision_ = PREC_F32;
-    try {
-      planned(B, st, body);
-    } catch (...) {
-      precision_ = keep;
-      throw;
-    }
-    precision_ = keep;
-    (void)range_hit(st);
+    l.prec_force = PREC_F32;
+    planned(B, st, body);
+    l.prec_force = -1;
+    (void)range_hit(l);
   }
 }
 
-// the fp16 range guard (common.h range_check): read and clear the device flag (synchronises `st`)
-bool Model::range_hit(hipStream_t st) {
+// the fp16 range guard (common.h range_check): read and clear the lane's device flag
+bool Model::range_hit(Lane& l) {
   int h = 0;
-  HIP_OK(hipMemcpyAsync(&h, rflag_, sizeof(int), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  if (h) HIP_OK(hipMemsetAsync(rflag_, 0, sizeof(int), st));
+  HIP_OK(hipMemcpyAsync(&h, l.rflag, sizeof(int), hipMemcpyDeviceToHost, l.st));
+  HIP_OK(hipStreamSynchronize(l.st));
+  if (h) HIP_OK(hipMemsetAsync(l.rflag, 0, sizeof(int), l.st));
   return h != 0;
 }
 
-// compress/decompress cannot fall back silently: the decoder has to reproduce the encoder's exact
-// entropy parameters, so both sides must run the same arithmetic
-void Model::range_fail(hipStream_t st) {
-  if (precision_ != PREC_F32 && range_hit(st))
-    throw Error("mlic: an activation exceeded the fp16 range of the split-fp16 kernels (|v| >= 65504); "
-                "encode and decode this input with set_precision(0) (exact fp32 MFMA)");
-}
+void Model::range_clear(Lane& l) { HIP_OK(hipMemsetAsync(l.rflag, 0, sizeof(int), l.st)); }
+
+// compress/decompress cannot fall back silently for the entropy model: the decoder has to reproduce
+// the encoder's exact entropy parameters, so both sides must run the same arithmetic
+static const char* kRangeMsg =
+    "mlic: an activation of the entropy model exceeded the fp16 range of the split-fp16 kernels (|v| >= 65504); "
+    "encode and decode this input with set_precision(0) (exact fp32 MFMA)";
 
 void Model::compress(const float* x, int B, int H, int W, const float* vbr_scales, hipStream_t st) {
   MLIC_CHECK(H % 64 == 0 && W % 64 == 0, "H and W must be multiples of 64");
@@ -1495,7 +1497,6 @@ void Model::compress(const float* x, int B, int H, int W, const float* vbr_scale
     compress_lane(x + first * img, cnt, H, W);
     for (int b = 0; b < cnt; ++b) enc_all_[first + b] = std::move(l.enc[b]);
   });
-  range_fail(st);
 }
 
 // mlicpp.py:199-290 for the lane's images: network on the lane stream, then one host thread per
@@ -1508,6 +1509,7 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   const int64_t ny = (int64_t)nph * B * n_per, nz = (int64_t)B * cfg_.N * hz * wz;
   int32_t *d_sym = nullptr, *d_idx = nullptr, *d_zsym = nullptr;
   double* d_bits = nullptr;  // [2][B]: -log2 likelihood sums of y and z per image (B1, rd_loss.py:42-45)
+  range_clear(l);
   planned(B, nullptr, [&] {
     d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
     d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
@@ -1543,6 +1545,7 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     HostStats::Scope w{hstats_.wait_ns};
     HIP_OK(hipStreamSynchronize(l.st));
   }
+  if (prec() != PREC_F32 && range_hit(l)) throw Error(kRangeMsg);
   l.enc.assign(B, EncodedImage{});
   for (int b = 0; b < B; ++b) {
     l.enc[b].y_bits = bits[b];
@@ -1591,7 +1594,6 @@ void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_
     set_vbr(vbr_scales ? vbr_scales + first : nullptr, cnt);
     decompress_lane(y + first, ylen + first, z + first, zlen + first, cnt, hz, wz, x_hat + first * img);
   });
-  range_fail(st);
 }
 
 // mlicpp.py:292-378 for the lane's images: z decoded on the host, then 20 phases of
@@ -1614,6 +1616,9 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
   }
   PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool());
   const int32_t* hz_sym = l.h_sym;
+  range_clear(l);
+  View yhat;
+  const View out{x_hat, 3, 16 * h, 16 * w, (int64_t)3 * 16 * h * 16 * w};
   planned(B, nullptr, [&] {
     int32_t* d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(B * zper));
     int32_t* d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(B * n_per));
@@ -1625,11 +1630,27 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
       HIP_OK(hipStreamSynchronize(l.st));  // the z symbols' host buffer is reused by the phase decoder
     }
     View hyper = h_s(zh);
-    View yhat = alloc(cfg_.M, h, w);
+    yhat = alloc(cfg_.M, h, w);
     slice_loop(Mode::Decode, hyper, nullptr, yhat, nullptr, d_sym, d_idx, &dec);
-    View out{x_hat, 3, 16 * h, 16 * w, (int64_t)3 * 16 * h * 16 * w};
+    // the entropy model (h_s + slice loop) must match the encoder's arithmetic: no fallback there
+    if (!l.dry && prec() != PREC_F32 && range_hit(l)) throw Error(kRangeMsg);
     g_s(yhat, out);
   });
+  if (prec() != PREC_F32 && range_hit(l)) {
+    // only the synthesis transform left fp16's range: y_hat is final, so re-run g_s alone in exact
+    // fp32 MFMA (as forward() re-runs), from a copy of y_hat (the re-plan may move the arena)
+    const size_t nb = sizeof(float) * (size_t)B * yhat.bs;
+    float* keep = nullptr;
+    HIP_OK(hipMalloc(&keep, nb));
+    struct Free {
+      float* p;
+      Lane& l;
+      ~Free() { l.prec_force = -1; (void)hipStreamSynchronize(l.st); (void)hipFree(p); }
+    } fr{keep, l};
+    HIP_OK(hipMemcpyAsync(keep, yhat.p, nb, hipMemcpyDeviceToDevice, l.st));
+    l.prec_force = PREC_F32;
+    planned(B, nullptr, [&] { g_s(View{keep, cfg_.M, h, w, yhat.bs}, out); });
+  }
 }
 
 // module-level entry points (tests): which in {local, chan, inter, intra, epa, epn, lrpa, lrpn, g_a, h_a, h_s, g_s, rbu}
@@ -1644,6 +1665,7 @@ void Model::run_module(const std::string& which, int i, const float* in0, const 
     ~Restore() { l.st = s; tl_lane_ = nullptr; }
   } restore{l, own};
   l.st = st;
+  range_clear(l);  // a stale hit of an earlier call must not be reported against this one
   planned(B, st, [&] {
     View a{const_cast<float*>(in0), Cin, H, W, (int64_t)Cin * H * W};
     View r;

@@ -124,6 +124,8 @@ struct Lane {
     std::string tag;
   };
   bool prof = false;
+  int* rflag = nullptr;  // this lane's device fp16 range flag (common.h range_check)
+  int prec_force = -1;   // >= 0: arithmetic override for this lane's current call (range-guard fallbacks)
   std::vector<ProfRec> recs;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -185,9 +187,10 @@ class Model {
   void add_hoist(const std::map<std::string, std::pair<const float*, int>>& ep0, hipStream_t st);
   ConvW make_conv(const float* w_dev, int Cout, int Cin, int K, const std::string& name, hipStream_t st);
   void add_chains(hipStream_t st);
-  int* rflag_ = nullptr;  // device fp16 range flag (common.h range_check)
-  bool range_hit(hipStream_t st);
-  void range_fail(hipStream_t st);
+  // the lane's fp16 range flag: read and clear (synchronises the lane stream), clear (stream-ordered)
+  bool range_hit(Lane& l);
+  void range_clear(Lane& l);
+  int prec() const { return L().prec_force >= 0 ? L().prec_force : precision_; }
   void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
                  const View* aux = nullptr, int H = 0, int W = 0);
   bool chain_on() const;

@@ -74,9 +74,13 @@ def _logits_cumulative(params, x):
     return logits
 
 
-@torch.no_grad()
-def bottleneck_tables(params: dict):
-    """compressai EntropyBottleneck.update(): (quantized_cdf, cdf_length, offset)."""
+def bottleneck_pmf(params: dict, sign_trick: bool = False):
+    """The per-channel pmf, tail mass, pmf lengths and offsets EntropyBottleneck.update() quantises.
+
+    compressai >= 1.2 (the reference pins 1.2.6, requirements.txt:31) takes the pmf from
+    `_likelihood(samples)`, i.e. the plain `sigmoid(upper) - sigmoid(lower)`.  `sign_trick=True` gives
+    the 1.1-era `abs(sigmoid(s*upper) - sigmoid(s*lower))`, s = -sign(lower + upper), kept only so a
+    test can count the quantised-CDF entries the two forms disagree on."""
     q = params["quantiles"].detach().cpu().float()
     p = {k: v.detach().cpu().float() for k, v in params.items()}
     medians = q[:, 0, 1]
@@ -89,9 +93,20 @@ def bottleneck_tables(params: dict):
     samples = torch.arange(max_length)[None, :] + pmf_start[:, None, None]
     lower = _logits_cumulative(p, samples - 0.5)
     upper = _logits_cumulative(p, samples + 0.5)
-    sign = -torch.sign(lower + upper)
-    pmf = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))[:, 0, :]
+    if sign_trick:
+        sign = -torch.sign(lower + upper)
+        pmf = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))
+    else:
+        pmf = torch.sigmoid(upper) - torch.sigmoid(lower)
+    pmf = pmf[:, 0, :]
     tail = torch.sigmoid(lower[:, 0, :1]) + torch.sigmoid(-upper[:, 0, -1:])
+    return pmf, tail, pmf_length, max_length, offset
+
+
+@torch.no_grad()
+def bottleneck_tables(params: dict, sign_trick: bool = False):
+    """compressai 1.2.6 EntropyBottleneck.update(): (quantized_cdf, cdf_length, offset)."""
+    pmf, tail, pmf_length, max_length, offset = bottleneck_pmf(params, sign_trick)
     cdf = _pmf_to_cdf(pmf, tail, pmf_length, max_length)
     return cdf, (pmf_length + 2).int(), offset.int()
 

@@ -353,12 +353,15 @@ class MLICPlusPlusVbr(MLICPlusPlus):
         self.lmbda = list(spec.VBR_LAMBDAS)
         self.levels = len(self.lmbda)
 
-    def _vbr_scales(self, B: int, stage: int = 2, s=1, inputscale=0, **kw) -> np.ndarray:
-        """mlicpp_vbr.py:122-137: scale = inputscale if given, else Gain[s] (clamped to the levels).
-        `s` / `inputscale` may be one value for the batch or one per image (BASELINE config 5)."""
+    def _vbr_scales(self, B: int, stage: int = 2, s=1, inputscale=0, coder: bool = False, **kw) -> np.ndarray:
+        """mlicpp_vbr.py:122-137: scale = inputscale if given, else Gain[s] (clamped to the levels);
+        the coder paths use |Gain[s]| (mlicpp_vbr.py:543, 899).  `s` / `inputscale` may be one value
+        for the batch or one per image (BASELINE config 5)."""
         if stage != 2:
             raise ValueError("only the inference stage (stage=2) is supported")
         g = self.Gain.detach().float().cpu().numpy()
+        if coder:
+            g = np.abs(g)
 
         def per_image(v):
             a = np.asarray(v.detach().cpu() if torch.is_tensor(v) else v).reshape(-1)
@@ -376,10 +379,10 @@ class MLICPlusPlusVbr(MLICPlusPlus):
         return super().forward(x, stage=stage, s=s, inputscale=inputscale)
 
     def compress(self, x, stage: int = 2, s=1, inputscale=0):
-        return super().compress(x, stage=stage, s=s, inputscale=inputscale)
+        return super().compress(x, stage=stage, s=s, inputscale=inputscale, coder=True)
 
     def decompress(self, strings, shape, stage: int = 2, s=1, inputscale=0):
-        return super().decompress(strings, shape, stage=stage, s=s, inputscale=inputscale)
+        return super().decompress(strings, shape, stage=stage, s=s, inputscale=inputscale, coder=True)
 
 
 def model_config(model_name: str = "MLICPP_S"):

@@ -135,15 +135,77 @@ def gen_modules():
          sd_sha=sd_checksum(sd))
 
 
+EB_SETS = [("MLICPP_L", None)] + [("MLICPP_L", r) for r in range(6)] + [
+    ("MLICPP_S", None), ("MLICPP_S", 1), ("MLICPP_S2", None), ("MLICPP_M", None), ("MLICPP_M_SMALL_DEC", None),
+    ("MLICPP_M_SMALL_DEC", 1), ("MLICPP_S_VBR", None), ("MLICPP_L_VBR", 2)]
+
+
+def gen_eb():
+    """EntropyBottleneck.update() tables (the z coder's CDFs) of every fixture weight set."""
+    arr = {}
+    for name, rate in EB_SETS:
+        m, sd = _ref_model(name, 0, rate)
+        m.update(force=True)
+        eb = m.entropy_bottleneck
+        tag = name + ("" if rate is None else f"_r{rate}")
+        arr[f"{tag}.quantized_cdf"] = eb.quantized_cdf
+        arr[f"{tag}.offset"] = eb.offset
+        arr[f"{tag}.cdf_length"] = eb.cdf_length
+        arr[f"{tag}.sd_sha"] = sd_checksum(sd)
+    save("eb_cdf_sets.npz", **arr)
+
+
+def _vbr_capture(m):
+    """Record, during one reference VBR forward (mlicpp_vbr.py:245-330, stage 2, no_quantoffset), the
+    input of every ste_round and the scaled scales handed to gaussian_conditional."""
+    mod = sys.modules[type(m).__module__]
+    rounds, gc_scales = [], []
+    orig = mod.ste_round
+
+    def rec_round(t):
+        rounds.append(t.detach().clone())
+        return orig(t)
+    mod.ste_round = rec_round
+    hook = m.gaussian_conditional.register_forward_hook(lambda mo, inp, out: gc_scales.append(inp[1].detach().clone()))
+    return rounds, gc_scales, lambda: (setattr(mod, "ste_round", orig), hook.remove())
+
+
+def vbr_streams(m, rounds, gc_scales):
+    """The coder inputs of a consistent VBR codec, from the reference forward's own values: phase
+    (slice i, anchor) codes round((y - mu) * scale) at the anchor cells in ckbd squeeze order
+    (utils/ckbd.py:47-73), with index build_indexes(scale * sigma) -- the indexes the reference's
+    compress_anchor_vbr computes (ckbd.py:81); its symbols (ckbd.py:87, which subtracts mu twice and
+    never scales) are the documented defect this replaces.  rounds[0] is the z rounding."""
+    ck = refload.load_module("utils/ckbd.py")
+    sym, idx = [], []
+    S = len(gc_scales)
+    assert len(rounds) == 1 + 2 * S, (len(rounds), S)
+    for i in range(S):
+        for ph, sq in ((0, ck.ckbd_anchor_sequeeze), (1, ck.ckbd_nonanchor_sequeeze)):
+            sym.append(torch.round(sq(rounds[1 + 2 * i + ph])).int().reshape(-1))
+            idx.append(m.gaussian_conditional.build_indexes(sq(gc_scales[i])).reshape(-1))
+    z_sym = torch.round(rounds[0]).int()
+    return torch.cat(sym).numpy(), torch.cat(idx).numpy().astype(np.int32), z_sym
+
+
 def gen_forward(name, H, W, seed=0, img_seed=0, s=None, with_streams=False, rate=None):
     m, sd = _ref_model(name, seed, rate)
     x = synthetic.synth_image(H, W, img_seed)
+    vbr_rec = None
+    if s is not None and with_streams:
+        vbr_rec = _vbr_capture(m)
     with torch.no_grad():
         out = m(x) if s is None else m(x, stage=2, s=s)
     yl, zl = out["likelihoods"]["y_likelihoods"], out["likelihoods"]["z_likelihoods"]
     bpp = float(sum(torch.log(l).sum() / (-math.log(2) * H * W) for l in (yl, zl)))
     arr = dict(x_hat=out["x_hat"], y_lik=yl, z_lik=zl, bpp=bpp, sd_sha=sd_checksum(sd), x_sha=t_checksum(x))
-    if with_streams:
+    if vbr_rec is not None:
+        rounds, gc_scales, undo = vbr_rec
+        undo()
+        m.update(force=True)
+        arr["y_symbols"], arr["y_indexes"], arr["z_symbols"] = vbr_streams(m, rounds, gc_scales)
+        arr["z_shape"] = np.asarray([H // 64, W // 64], np.int32)
+    elif with_streams:
         m.update(force=True)
         enc_mod = sys.modules[type(m).__module__]
         captured = {}
@@ -168,7 +230,14 @@ def gen_forward(name, H, W, seed=0, img_seed=0, s=None, with_streams=False, rate
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    what = sys.argv[1:] or ["bitexact", "modules", "forward", "rates"]
+    what = sys.argv[1:] or ["bitexact", "modules", "forward", "rates", "eb", "svbr"]
+    if "eb" in what:
+        gen_eb()
+    if "svbr" in what:
+        # MLICPP_S_VBR, the VBR name the reference factory registers (models/model_loader.py:12-13)
+        for s in (0, 3, 5):
+            gen_forward("MLICPP_S_VBR", 128, 128, s=s, with_streams=True)
+        gen_forward("MLICPP_S_VBR", 192, 256, img_seed=3, s=1, with_streams=True)
     if "bitexact" in what:
         gen_bitexact()
     if "modules" in what:

@@ -238,10 +238,11 @@ class EntropyBottleneck(EntropyModel):
         samples = samples[None, :] + pmf_start[:, None, None]
         half = float(0.5)
         with torch.no_grad():
+            # compressai 1.2.x: pmf, lower, upper = self._likelihood(samples, stop_gradient=True),
+            # i.e. the plain sigmoid difference (1.1.x used the sign trick with abs)
             lower = self._logits_cumulative(samples - half, stop_gradient=True)
             upper = self._logits_cumulative(samples + half, stop_gradient=True)
-            sign = -torch.sign(lower + upper)
-            pmf = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))
+            pmf = torch.sigmoid(upper) - torch.sigmoid(lower)
             pmf = pmf[:, 0, :]
             tail_mass = torch.sigmoid(lower[:, 0, :1]) + torch.sigmoid(-upper[:, 0, -1:])
         self._quantized_cdf = self._pmf_to_cdf(pmf, tail_mass, pmf_length, max_length)

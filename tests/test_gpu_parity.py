@@ -110,7 +110,8 @@ def test_module_vectors(golden):
 
 FWD = [("MLICPP_L", 128, 192, None), ("MLICPP_L", 128, 128, None), ("MLICPP_S", 128, 128, None),
        ("MLICPP_S2", 128, 128, None), ("MLICPP_M", 128, 128, None), ("MLICPP_M_SMALL_DEC", 128, 128, None),
-       ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5)]
+       ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5),
+       ("MLICPP_S_VBR", 128, 128, 0), ("MLICPP_S_VBR", 128, 128, 3), ("MLICPP_S_VBR", 128, 128, 5)]
 
 
 @pytest.mark.parametrize("name,H,W,s", FWD)
@@ -150,21 +151,26 @@ def test_forward_matches_oracle_batched(name, B, H, W):
     assert_xhat_close(out["x_hat"].cpu(), o["x_hat"])
 
 
-@pytest.mark.parametrize("name,H,W", [("MLICPP_L", 128, 192), ("MLICPP_S", 128, 128),
-                                      ("MLICPP_M_SMALL_DEC", 128, 128)])
-def test_compress_streams_match_reference(golden, name, H, W):
-    """Coder inputs vs the exact symbol/index lists the reference hands to its rANS encoder.
+@pytest.mark.parametrize("name,H,W,s,img", [("MLICPP_L", 128, 192, None, 0), ("MLICPP_S", 128, 128, None, 0),
+                                            ("MLICPP_M_SMALL_DEC", 128, 128, None, 0), ("MLICPP_S_VBR", 128, 128, 0, 0),
+                                            ("MLICPP_S_VBR", 128, 128, 3, 0), ("MLICPP_S_VBR", 128, 128, 5, 0),
+                                            ("MLICPP_S_VBR", 192, 256, 1, 3)])
+def test_compress_streams_match_reference(golden, name, H, W, s, img):
+    """Coder inputs vs the exact symbol/index lists the reference hands to its rANS encoder (VBR: the
+    values a consistent codec codes, taken from the reference forward, oracle/gen_golden.py).
     fp32 summation order may flip a rounding decision, so allow a tiny mismatch fraction."""
-    g = golden(f"forward_{name}_{H}x{W}.npz")
+    tag = f"{name}_{H}x{W}" + ("" if s is None else f"_s{s}")
+    g = golden(f"forward_{tag}.npz")
     net = net_for(name)
     net.update()
-    x = synthetic.synth_image(H, W, 0).to(DEV)
-    c = net.compress(x)
+    x = synthetic.synth_image(H, W, img).to(DEV)
+    kw = {} if s is None else {"stage": 2, "s": s}
+    c = net.compress(x, **kw)
     ys, yi, zs = net.encoded_streams(0)
     assert ys.shape == g["y_symbols"].shape
     rec = {"y_n": int(ys.size), "y_symbol_mismatch": int((ys != g["y_symbols"]).sum()),
            "y_index_mismatch": int((yi != g["y_indexes"]).sum())}
-    PARITY[f"streams_{name}_{H}x{W}"] = rec
+    PARITY[f"streams_{tag}"] = rec
     assert rec["y_symbol_mismatch"] <= rec["y_n"] * 1e-3, rec
     assert rec["y_index_mismatch"] <= rec["y_n"] * 1e-3, rec
     assert np.array_equal(zs, g["z_symbols"].reshape(-1))
@@ -173,11 +179,14 @@ def test_compress_streams_match_reference(golden, name, H, W):
     dec = entropy.rans_decode(c["strings"][0][0], yi, gc._quantized_cdf.cpu(), gc._cdf_length.cpu(),
                               gc._offset.cpu())
     assert np.array_equal(dec, ys)
+    if s is not None:  # and the streams decode back to the forward x_hat
+        d = net.decompress(c["strings"], c["shape"], **kw)
+        assert torch.equal(d["x_hat"], net(x, **kw)["x_hat"])
 
 
 @pytest.mark.parametrize("name,B,H,W,s", [("MLICPP_L", 1, 128, 192, None), ("MLICPP_L", 2, 128, 128, None),
                                           ("MLICPP_S", 1, 192, 128, None), ("MLICPP_M_SMALL_DEC", 1, 128, 128, None),
-                                          ("MLICPP_L_VBR", 1, 128, 128, 2)])
+                                          ("MLICPP_L_VBR", 1, 128, 128, 2), ("MLICPP_S_VBR", 2, 128, 192, 4)])
 def test_roundtrip_bitexact(name, B, H, W, s):
     """decompress(compress(x)).x_hat == forward(x).x_hat, bit for bit (same kernels, same ŷ)."""
     net = net_for(name)
@@ -271,6 +280,7 @@ def test_file_format_roundtrip(tmp_path):
     path = str(tmp_path / "img.bin")
     n = bitstream.write_file(path, 120, 200, out)
     assert os.path.getsize(path) == n == r["bytes"]
+    assert n == bitstream.file_bytes(len(out["strings"][0][0]), len(out["strings"][1][0]))
     hdr, strings, shape = bitstream.read_file(path)
     assert tuple(hdr) == (120, 200) and strings == [[out["strings"][0][0]], [out["strings"][1][0]]]
 
@@ -527,6 +537,36 @@ def test_fp16_range_guard():
     net.update()
     with pytest.raises(_lib.MlicError, match="fp16 range"):
         net.compress(x)
+
+
+def test_fp16_range_guard_synthesis_only():
+    """An activation beyond fp16 inside g_s only (a synthesis weight scaled up): forward() falls back to
+    exact fp32; compress() (no g_s) is unaffected; decompress() keeps the split-fp16 entropy model the
+    encoder used and re-runs only g_s in exact fp32 -- it decodes instead of refusing the stream."""
+    name, H, W = "MLICPP_S", 128, 128
+    sd = synthetic.synth_state_dict(name, rate=1)
+    k = "g_s.synthesis_transform.0.conv1.point_conv.weight"
+    sd[k] = sd[k] * 5000
+    net = get_model(name)
+    net.load_state_dict(sd)
+    net = net.to(DEV).eval()
+    x = synthetic.synth_image(H, W, 4).to(DEV)
+    f = net(x)
+    net.set_precision(0)
+    f0 = net(x)
+    net.set_precision(2)
+    assert torch.isfinite(f["x_hat"]).all() and torch.equal(f["x_hat"], f0["x_hat"])
+    net.update()
+    c = net.compress(x)
+    d = net.decompress(c["strings"], c["shape"])
+    xd, xf = d["x_hat"].double(), f["x_hat"].double()
+    assert torch.isfinite(xd).all()
+    rel = float((xd - xf).abs().mean() / xf.abs().mean().clamp_min(1e-12))
+    PARITY["range_guard_gs_only"] = {"decode_vs_fp32_forward_mean_rel": rel}
+    assert rel <= 1e-3, rel
+    # and the same stream decoded again gives the same image (the fallback is deterministic)
+    d2 = net.decompress(c["strings"], c["shape"])
+    assert torch.equal(d2["x_hat"], d["x_hat"])
 
 
 @pytest.mark.parametrize("name,rate,H,W", [("MLICPP_L", 2, 1088, 1920), ("MLICPP_S", 2, 512, 768),

@@ -62,15 +62,55 @@ def test_gaussian_tables_match_reference_update(golden):
     assert np.array_equal(offset.numpy(), g["offset"])
 
 
+def _eb_params(sd):
+    return {k.split(".", 1)[1]: v for k, v in sd.items() if k.startswith("entropy_bottleneck.")
+            and (".quantiles" in k or "._" in k) and not k.endswith(("_offset", "_quantized_cdf", "_cdf_length"))}
+
+
 def test_bottleneck_tables_match_reference_update(golden):
     g = golden("eb_cdf_L.npz")
     sd = synthetic.synth_state_dict("MLICPP_L", 0)
-    params = {k.split(".", 1)[1]: v for k, v in sd.items() if k.startswith("entropy_bottleneck.")
-              and (".quantiles" in k or "._" in k) and not k.endswith(("_offset", "_quantized_cdf", "_cdf_length"))}
-    cdf, length, offset = entropy.bottleneck_tables(params)
+    cdf, length, offset = entropy.bottleneck_tables(_eb_params(sd))
     assert np.array_equal(cdf.numpy(), g["quantized_cdf"])
     assert np.array_equal(length.numpy(), g["cdf_length"])
     assert np.array_equal(offset.numpy(), g["offset"])
+
+
+def test_bottleneck_tables_every_weight_set_and_form_diff(golden):
+    """EntropyBottleneck.update() (mlicpp.py:470-475 -> compressai 1.2.6) on every fixture weight set:
+    the product's z CDF tables equal the reference's, entry for entry.  Also counts how many quantised
+    CDF entries the compressai-1.1 sign-trick pmf would change -- the entries where a coder built on the
+    wrong form would write z streams a reference decoder cannot read (recorded in $MLIC_PARITY_OUT)."""
+    import hashlib
+    import json
+    g = golden("eb_cdf_sets.npz")
+    tags = sorted({k.split(".")[0] for k in g.files})
+    assert len(tags) >= 10
+    rec = {}
+    for tag in tags:
+        name, rate = (tag.rsplit("_r", 1)[0], int(tag.rsplit("_r", 1)[1])) if "_r" in tag[-3:] else (tag, None)
+        sd = synthetic.synth_state_dict(name, 0, rate=rate)
+        h = hashlib.sha256()
+        for k in sorted(sd):
+            h.update(k.encode())
+            h.update(sd[k].contiguous().numpy().tobytes())
+        assert h.hexdigest() == str(g[f"{tag}.sd_sha"]), tag
+        p = _eb_params(sd)
+        cdf, length, offset = entropy.bottleneck_tables(p)
+        assert np.array_equal(cdf.numpy(), g[f"{tag}.quantized_cdf"]), tag
+        assert np.array_equal(length.numpy(), g[f"{tag}.cdf_length"]), tag
+        assert np.array_equal(offset.numpy(), g[f"{tag}.offset"]), tag
+        old, _, _ = entropy.bottleneck_tables(p, sign_trick=True)
+        diff = old.numpy() != cdf.numpy()
+        rec[tag] = {"entries": int(cdf.numel()), "sign_trick_entries_differing": int(diff.sum()),
+                    "channels_differing": int(diff.any(axis=1).sum()), "channels": int(cdf.shape[0])}
+    out = os.environ.get("MLIC_PARITY_OUT")
+    if out:
+        old_rec = json.load(open(out)) if os.path.exists(out) else {}
+        old_rec["eb_cdf_form_diff"] = rec
+        with open(out, "w") as f:
+            json.dump(old_rec, f, indent=1, sort_keys=True)
+    print(json.dumps(rec))
 
 
 def _gc_tables(golden):
@@ -149,3 +189,17 @@ def test_conv_choice_pins_the_measured_selection():
     assert choice(3, 192, 1088, 1920, 1, stride=2) == SMALLCIN
     assert choice(192, 12, 544, 960, 3) == NARROW
     assert choice(48, 48, 1088, 1920, 1) == PW            # small-decoder g_s width
+
+
+@pytest.mark.parametrize("vbr", [False, True])
+def test_file_bytes_is_the_written_file_size(vbr):
+    """bench.py's bpp_file counts the whole file the harness writes (utils/utils.py:71-83)."""
+    import io
+    from mlic_amd import bitstream
+    y, z = b"\x01" * 37, b"\x02" * 5
+    buf = io.BytesIO()
+    n = bitstream.write_stream(buf, 120, 200, (2, 4), [[y], [z]], level=3 if vbr else None)
+    assert n == len(buf.getvalue()) == bitstream.file_bytes(len(y), len(z), vbr=vbr)
+    buf.seek(0)
+    hdr, strings, shape = bitstream.read_stream(buf, vbr=vbr)
+    assert strings == [[y], [z]] and shape == (2, 4) and hdr[:2] == (120, 200)

@@ -79,7 +79,8 @@ def test_module_vectors(golden):
 
 FWD = [("MLICPP_L", 128, 192, None), ("MLICPP_L", 128, 128, None), ("MLICPP_S", 128, 128, None),
        ("MLICPP_S2", 128, 128, None), ("MLICPP_M", 128, 128, None), ("MLICPP_M_SMALL_DEC", 128, 128, None),
-       ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5)]
+       ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5),
+       ("MLICPP_S_VBR", 128, 128, 0), ("MLICPP_S_VBR", 128, 128, 3), ("MLICPP_S_VBR", 128, 128, 5)]
 
 
 @pytest.mark.parametrize("name,H,W,s", FWD)
@@ -103,20 +104,28 @@ def test_forward_matches_reference(golden, name, H, W, s):
     assert abs(ref.psnr_uint8(x, out["x_hat"]) - psnr_ref) < 0.01
 
 
-@pytest.mark.parametrize("name,H,W", [("MLICPP_L", 128, 192), ("MLICPP_S", 128, 128), ("MLICPP_M_SMALL_DEC", 128, 128)])
-def test_compress_streams_match_reference(golden, name, H, W):
-    g = golden(f"forward_{name}_{H}x{W}.npz")
+@pytest.mark.parametrize("name,H,W,s,img", [("MLICPP_L", 128, 192, None, 0), ("MLICPP_S", 128, 128, None, 0),
+                                            ("MLICPP_M_SMALL_DEC", 128, 128, None, 0), ("MLICPP_S_VBR", 128, 128, 0, 0),
+                                            ("MLICPP_S_VBR", 128, 128, 3, 0), ("MLICPP_S_VBR", 128, 128, 5, 0),
+                                            ("MLICPP_S_VBR", 192, 256, 1, 3)])
+def test_compress_streams_match_reference(golden, name, H, W, s, img):
+    """Coder inputs (y symbols / indexes, z symbols) vs the reference's.  VBR: the fixture holds the
+    values a consistent codec codes, taken from the reference forward itself (oracle/gen_golden.py
+    vbr_streams; the reference's own VBR compress is defective)."""
+    g = golden(f"forward_{name}_{H}x{W}" + ("" if s is None else f"_s{s}") + ".npz")
     sd = synthetic.synth_state_dict(name, 0)
     m = ref.RefMLIC(name, sd)
-    x = synthetic.synth_image(H, W, 0)
-    st = m.compress_streams(x)
+    x = synthetic.synth_image(H, W, img)
+    assert hashlib.sha256(x.numpy().tobytes()).hexdigest() == str(g["x_sha"])
+    kw = {} if s is None else {"s": s}
+    st = m.compress_streams(x, **kw)
     sym = torch.cat([p[0].reshape(-1) for p in st["phases"]]).numpy()
     idx = torch.cat([p[1].reshape(-1) for p in st["phases"]]).numpy()
     assert np.array_equal(st["z_symbols"].numpy(), g["z_symbols"])
     assert np.array_equal(idx, g["y_indexes"])
     assert np.array_equal(sym, g["y_symbols"])
     # decode from the streams reproduces the forward x_hat (round trip invariant)
-    dec = m.decode_streams(st["z_symbols"], [p[0] for p in st["phases"]])
+    dec = m.decode_streams(st["z_symbols"], [p[0] for p in st["phases"]], **kw)
     assert torch.equal(dec["y_hat"], st["y_hat"])
     close(dec["x_hat"], g["x_hat"], rtol=1e-4, atol=1e-4)
 
