@@ -104,6 +104,13 @@ def parse():
                          "steps' and rocprofv3's per-kernel averages; 1 = isolated per-kernel times)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
                     help="PMC-derived HBM bytes per launch of the dominant family (tools/pmc_traffic.py)")
+    ap.add_argument("--group-concurrency", type=int, default=4,
+                    help="(weights, shape) batches of a step run concurrently, each on its own model "
+                         "instance, lanes and stream (1 = one after another)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="run rank --emulate-rank's share of a W-rank job list on this one GPU, with 1/W of "
+                         "the host cores (a prediction of one rank of a W-GPU run; value = that rank's img/s)")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     return ap.parse_args()
 
 
@@ -121,10 +128,11 @@ def build_jobs(a, rank: int, world: int):
     wl = WORKLOADS[a.config]
     rate = None if a.rate < 0 else a.rate
     if a.config == "kodak-sweep":
-        # 24 Kodak-size images (the set has 4 portrait members) x 6 weight sets = 144 jobs
+        # 24 Kodak-size images (the set has 4 portrait members) x 6 weight sets = 144 jobs,
+        # cut into contiguous runs of (weight set, shape) batches: whole batches per rank
         shapes = [(512, 768)] * 20 + [(768, 512)] * 4
         alljobs = [Job(r * 24 + i, wl["model"], r, H, W, 2000 + i, r) for r in range(6) for i, (H, W) in enumerate(shapes)]
-        mine = mdist.lpt_shard([(j.H, j.W) for j in alljobs], world)[rank]
+        mine = mdist.group_shard([(j.rate, j.H, j.W) for j in alljobs], [(j.H, j.W) for j in alljobs], world)[rank]
         return [alljobs[i] for i in mine], len(alljobs)
     groups = wl["groups"]
     if a.batch > 0 and len(groups) == 1:
@@ -223,31 +231,44 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    emulated = a.emulate_world > 1
+    if emulated:
+        assert not distributed and 0 <= a.emulate_rank < a.emulate_world, "--emulate-world runs one process"
+    # the job list's world / rank, and this process's slot among the node's ranks
+    jworld, jrank = (a.emulate_world, a.emulate_rank) if emulated else (world, rank)
+    nloc = a.emulate_world if emulated else int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    lslot = a.emulate_rank if emulated else local
+    # host cores per rank, before any GPU call: the ranks of a node split its cores into contiguous
+    # slices (pinned), and the entropy-coder pool of each rank gets its slice ($MLIC_HOST_THREADS, read
+    # at first use)
+    cores = sorted(os.sched_getaffinity(0))
+    if nloc > 1 and len(cores) >= 2 * nloc:
+        k = len(cores) // nloc
+        cores = cores[lslot * k:(lslot + 1) * k]
+        os.sched_setaffinity(0, cores)
+    if "MLIC_HOST_THREADS" not in os.environ:
+        os.environ["MLIC_HOST_THREADS"] = str(max(2, min(16, len(cores))))
     if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    # host cores per rank: the ranks of a node split its cores into contiguous slices (pinned), and the
-    # entropy-coder pool of each rank gets its slice ($MLIC_HOST_THREADS, read at first use)
-    nloc = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    cores = sorted(os.sched_getaffinity(0))
-    if nloc > 1 and len(cores) >= 2 * nloc:
-        k = len(cores) // nloc
-        cores = cores[local * k:(local + 1) * k]
-        os.sched_setaffinity(0, cores)
-    if "MLIC_HOST_THREADS" not in os.environ:
-        os.environ["MLIC_HOST_THREADS"] = str(max(2, min(16, len(cores))))
 
     from mlic_amd import _lib, bitstream, get_model, synthetic
     from mlic_amd import dist as mdist
     wl = WORKLOADS[a.config]
-    jobs, n_jobs_total = build_jobs(a, rank, world)
+    jobs, n_jobs_total = build_jobs(a, jrank, jworld)
     groups = batches(jobs)
+    # biggest batches first: the concurrent groups finish together
+    order = sorted(range(len(groups)), key=lambda gi: -len(groups[gi][1]) * groups[gi][0][2] * groups[gi][0][3])
+    conc = max(1, min(a.group_concurrency, len(groups)))
 
-    nets = {}
-    for (model, rate, _, _), _js in groups:
-        if (model, rate) not in nets:
+    # one model instance per group when groups run concurrently (a handle's lanes serve one call at a
+    # time), one per weight set otherwise
+    nets, gnet = {}, []
+    for gi, ((model, rate, _, _), _js) in enumerate(groups):
+        key = (model, rate, gi if conc > 1 else 0)
+        if key not in nets:
             n = get_model(model)
             n.load_state_dict(synthetic.synth_state_dict(model, 0, rate=rate))
             n = n.to(dev).eval()
@@ -255,26 +276,40 @@ def main():
             n.set_lanes(a.lanes)
             n.set_precision(a.precision)
             n.set_synthesis_precision(1 if a.synth_fp16 else 0)
-            nets[(model, rate)] = n
+            nets[key] = n
+        gnet.append(nets[key])
     # inputs resident in HBM before the timed region
     xs = [torch.cat([synthetic.synth_image(j.H, j.W, j.seed) for j in js]).to(dev) for _, js in groups]
+    streams = [torch.cuda.Stream(dev) for _ in groups]
+    torch.cuda.synchronize()
     is_vbr = wl["model"].endswith("_VBR")
 
     split = {"compress": 0.0, "decompress": 0.0}
     last = {}
 
-    def step():
-        for gi, ((model, rate, H, W), js) in enumerate(groups):
-            net = nets[(model, rate)]
-            kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
+    def run_group(gi):
+        (model, rate, H, W), js = groups[gi]
+        net = gnet[gi]
+        kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
+        with torch.cuda.stream(streams[gi]):
             t_a = time.perf_counter()
             c = net.compress(xs[gi], **kw)
             t_b = time.perf_counter()
             d = net.decompress(c["strings"], c["shape"], **kw)
             t_c = time.perf_counter()
-            split["compress"] += t_b - t_a
-            split["decompress"] += t_c - t_b
-            last[gi] = (c, d, (t_b - t_a) / len(js), (t_c - t_b) / len(js))
+        last[gi] = (c, d, (t_b - t_a) / len(js), (t_c - t_b) / len(js))
+        return t_b - t_a, t_c - t_b
+
+    pool = None
+    if conc > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(conc)
+
+    def step():
+        res = list(pool.map(run_group, order)) if pool else [run_group(gi) for gi in order]
+        for te, td in res:
+            split["compress"] += te
+            split["decompress"] += td
 
     for _ in range(a.warmup):
         step()
@@ -312,9 +347,9 @@ def main():
     r = 0
     for gi, ((model, rate, H, W), js) in enumerate(groups):
         c, d, enc_s, dec_s = last[gi]
-        net = nets[(model, rate)]
+        net = gnet[gi]
         mses = mse_u8(xs[gi], d["x_hat"])
-        if len(groups) > 1:
+        if gnet.count(net) > 1:
             # the device-side likelihood bits belong to a net's last compress(): groups sharing one
             # net (vbr-mixed's 4K + 1080p) re-run this group's compress, untimed, to read them
             kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
@@ -349,10 +384,13 @@ def main():
     roofline = None
     prof = {}
     if not a.no_roofline:
-        roofline, prof = profile_roofline(a, nets, groups, xs, is_vbr, elapsed / a.steps, dev)
+        roofline, prof = profile_roofline(a, gnet, groups, xs, is_vbr, elapsed / a.steps, dev)
 
     if rank == 0:
-        images = n_jobs_total * a.steps if wl["scaling"] == "strong" else len(jobs) * world * a.steps
+        if emulated:  # this rank's images only: a per-GPU prediction
+            images = len(jobs) * a.steps
+        else:
+            images = n_jobs_total * a.steps if wl["scaling"] == "strong" else len(jobs) * world * a.steps
         q = allrec.numpy()
         quality = {"bpp_file_mean": round(float(q[:, F["bpp_file"]].mean()), 5),
                    "bpp_lik_mean": round(float(q[:, F["bpp_lik"]].mean()), 5),
@@ -395,8 +433,14 @@ def main():
             "host_threads": int(os.environ.get("MLIC_HOST_THREADS", "0")),
             "wall_ms_per_step": wall_split,
             "lanes": a.lanes,
+            "group_concurrency": conc,
+            "batches_per_step": [len(js) for _, js in groups],
             "quality": quality,
         }
+        if emulated:
+            out["emulated"] = {"world": a.emulate_world, "rank": a.emulate_rank, "host_cores": len(cores),
+                               "note": "one rank's job list of a W-GPU run on one GPU with 1/W of the host cores; "
+                                       "value = that rank's images/s (per-GPU)"}
         if world == 1 and not a.no_cpu_baseline:
             j0 = jobs[0]
             sH, sW = (j0.H, j0.W) if j0.H * j0.W <= 1088 * 1920 else (1088, 1920)
@@ -404,7 +448,7 @@ def main():
             if a.config == "kodak-sweep":
                 out["quality"]["delta_vs_cpu_oracle"] = oracle_deltas(
                     wl["model"], sorted({k[1] for k, _ in groups}), 512, 768,
-                    {k[1]: nets[k[:2]] for k, _ in groups}, dev)
+                    {k[1]: gnet[gi] for gi, (k, _) in enumerate(groups)}, dev)
         else:
             out["cpu_baseline"] = None
         if a.records_out:
@@ -416,7 +460,7 @@ def main():
         dist.destroy_process_group()
 
 
-def profile_roofline(a, nets, groups, xs, is_vbr, t_step_s, dev):
+def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev):
     from mlic_amd import _lib
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
@@ -430,7 +474,7 @@ def profile_roofline(a, nets, groups, xs, is_vbr, t_step_s, dev):
         fam = {}
         layer_rows = []
         for gi, ((model, rate, H, W), js) in enumerate(groups):
-            net = nets[(model, rate)]
+            net = gnet[gi]
             h = net._handle
             _lib.call("mlic_set_lanes", h, lanes)
             _lib.call("mlic_set_profiling", h, 1)

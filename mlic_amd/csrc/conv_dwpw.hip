@@ -1,23 +1,30 @@
-// Fused depthwise-separable conv ("dwpw"): the fork's DepthWiseConv (modules/layers/conv.py:22-32:
-// depthwise 3x3 stride 1 pad 1 + bias, then pointwise 1x1 + bias, then the block's epilogue) in ONE
-// kernel, so the depthwise output never goes to HBM.  g_a / g_s run it on every stride-1 dwsep conv
-// of their residual blocks (res_blk.py ResidualBlock conv1/conv2, ResidualBlockWithStride conv2,
-// ResidualBlockUpsample conv): Cin = Cout = N.
+// Fused depthwise-separable conv ("dwpw"): the fork's DepthWiseConv (modules/layers/conv.py:22-32 and
+// 46-63: depthwise 3x3 stride 1 pad 1 + bias, then pointwise 1x1 + bias, then the block's GELU /
+// residual) in ONE kernel, so the depthwise output never goes to HBM.  g_a / g_s run it on every
+// stride-1 dwsep conv of their residual blocks (res_blk.py:62-154: ResidualBlock conv1 / conv2,
+// ResidualBlockWithStride conv2, ResidualBlockUpsample conv): Cin = Cout = N.
 //
-// Block = 8 rows x 32 columns of one image, 8 waves (wave w: row y0 + w, lane l32: column x0 + l32,
-// lane half h: channels 8h..8h+7 of a 16-channel k-step -- the B fragment of
-// v_mfma_f32_32x32x16_f16), all Cout rows per wave.  Per k-step, through a 2-slot LDS ring:
-//   * the input patch, 16 channels x 10 rows x 34 columns (the block + its 1-pixel halo), staged
-//     through registers by coalesced buffer loads (out-of-image positions read 0 via an
-//     out-of-range offset) one k-step ahead and stored with ds_write_b32;
-//   * the k-step's pointwise weights, split hi/lo, 64-byte rows [hi k0-7 | hi k8-15 | lo | lo] with
-//     the 16-byte granule XOR-swizzled by (row >> 2) & 3 (conflict-free ds_read_b128 A fragments),
-//     staged the same way from the L2-resident split weights;
-// and the depthwise taps + bias stay resident ([C][12] floats, broadcast ds_read_b128).  The
-// depthwise sum is acc = 0, 9 taps row-major by fma, + bias (dw3x3's order: the fused B operand
-// equals the unfused depthwise output bit for bit), then the hi/lo split in registers; one barrier
-// per k-step.  A persistent grid walks the blocks; the staging stream runs across block boundaries.
-// HBM bytes per pixel: 4 * (Cin + Cout [+ Cout residual]) -- the pointwise conv's alone.
+// Barrier-free form of the resident pointwise kernel (conv_pw.hip pw_resident_kernel).  One workgroup
+// per CU keeps, for its whole life, in LDS:
+//   * the split hi/lo pointwise weights as an MFMA A-fragment image, [k-step][row][64 B] with the four
+//     16-byte granules (hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15) XOR-swizzled by (row >> 2) & 3:
+//     conflict-free ds_read_b128 for both lane groups (no padding, so N = 192 fits beside the taps);
+//   * the depthwise taps + bias, [C][12] floats, read by broadcast ds_read_b128.
+// Each of its 8 waves then walks its own 32-pixel row segments with no workgroup barrier (the waves of a
+// workgroup take the 8 rows of one 8 x 32 tile, so a row's three readers share the CU's L1): lane l32 is
+// column x0 + l32, lane half h holds channels 8h..8h+7 of a 16-deep k-step (the B fragment of
+// v_mfma_f32_32x32x16_f16).  Per channel the lane loads its column of the 3 input rows, and its
+// horizontal neighbours come from the adjacent lanes by DPP row shifts; the lanes at the ends of each
+// 16-lane DPP row take the neighbour from a second (edge) load whose address only they need
+// (x - 1 at columns 0 / 16, x + 1 at columns 15 / 31).  Out-of-image taps read 0 through an
+// out-of-range buffer offset.  The depthwise sum is dw3x3_s1_vec_kernel's order (acc = 0, taps
+// row-major by fma, + bias), so the B operand equals the unfused depthwise output bit for bit, and
+// the MFMA k order is pw_resident's: the fused output equals depthwise + resident pointwise bit for
+// bit (tests/test_gpu_conv.py::test_dwpw_fused).  Loads run one k-step ahead in a register ring that
+// carries across row segments.  Tiles are dealt XCD-aware: the workgroups of one XCD (blockIdx % 8
+// under round-robin placement; speed only) take one contiguous eighth of them.
+// HBM bytes per pixel: 4 * (Cin + Cout [+ Cout residual]) -- the pointwise conv's alone; the unfused
+// pair moves 4 * (3 Cin + Cout [+ Cout]).
 #include "common.h"
 #include "kernels.h"
 
@@ -28,18 +35,13 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DP_WAVES = 8;
-constexpr int DP_THREADS = DP_WAVES * 64;
-constexpr int DP_TW = 32;                      // block columns
-constexpr int DP_PR = DP_WAVES + 2;            // patch rows
-constexpr int DP_PC = DP_TW + 2;               // patch columns
-constexpr int DP_CH = DP_PR * DP_PC;           // floats per channel plane of the patch
-constexpr int DP_KC = 32;                     // channels per k-step (two 16-deep MFMA k-slices)
-constexpr int DP_PSZ = DP_KC * DP_CH;          // floats per k-step patch
-constexpr int DP_DWP = 12;                     // floats per depthwise channel: 9 taps, bias, 2 pad
-constexpr uint32_t DP_OOB = 0x80000000u;       // buffer offset past any image: the load returns 0
+constexpr int DR_WAVES = 8;
+constexpr int DR_THREADS = DR_WAVES * 64;
+constexpr int DR_DWP = 12;                 // floats per depthwise channel in LDS: 9 taps, bias, 2 pad
+constexpr uint32_t DR_OOB = 0x80000000u;   // buffer offset past any image: the load returns 0
+constexpr int DPP_ROW_SHL1 = 0x101, DPP_ROW_SHR1 = 0x111;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t dp_rsrc(const float* base, uint32_t bytes) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dr_rsrc(const float* base, uint32_t bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
@@ -47,178 +49,183 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dp_rsrc(const float* base, uin
   return __builtin_amdgcn_make_buffer_rsrc(pb, 0, bytes, 0x00020000);
 }
 
-__device__ __forceinline__ void dp_opaque(uint32_t& v) { asm volatile("" : "+s"(v)); }
-}  // namespace
+__device__ __forceinline__ void dr_opaque(uint32_t& v) { asm volatile("" : "+s"(v)); }
+__device__ __forceinline__ int dr_swz(int row) { return (row >> 2) & 3; }
 
-#ifdef MLIC_DP_TRACE  // diagnostic builds (tools/gpu/dwpw_probe.hip): phase stamps of workgroup 0
-__device__ unsigned long long* g_dp_trace;
-#define DP_TR(slot) \
-  if (blockIdx.x == 0 && threadIdx.x < 64 && (slot) < 512) tr[(slot)] = __builtin_readcyclecounter()
-#else
-#define DP_TR(slot)
-#endif
-namespace {
-__device__ __forceinline__ int dp_swz(int row) { return (row >> 1) & 7; }
+// neighbour of this lane's value from lane - 1 (SHR) / lane + 1 (SHL) of its 16-lane DPP row; the
+// first / last lane of the row keeps `edge`
+template <int CTRL>
+__device__ __forceinline__ float dpp_nb(float edge, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, edge), __builtin_bit_cast(int, v),
+                                                                CTRL, 0xF, 0xF, false));
+}
 }  // namespace
 
 template <int CIN, int CT, bool GELU, bool RES>
-__global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _Float16* __restrict__ wh,
+__global__ __launch_bounds__(DR_THREADS) void dwpw_kernel(ConvParams P, const _Float16* __restrict__ wh,
                                                         const _Float16* __restrict__ wl, int cin_pad,
                                                         const float* __restrict__ dww, const float* __restrict__ dwb) {
-  constexpr int KS = CIN / DP_KC;
+  constexpr int KS = CIN / 16;
   constexpr int ROWS = CT * 32;
-  constexpr int WSZ = ROWS * 128;                      // bytes per k-step weight slot
-  constexpr int NWQ = ROWS * 8;                        // 16-byte weight chunks per k-step
-  constexpr int NWL = (NWQ + DP_THREADS - 1) / DP_THREADS;
-  constexpr int LDS = 2 * DP_PSZ * 4 + 2 * WSZ + CIN * DP_DWP * 4 + ROWS * 4;
-  static_assert(LDS <= 160 * 1024, "dwpw LDS");
+  constexpr int TAPB = CIN * DR_DWP * 4 + ROWS * 4;  // taps + bias first: small ds_read offsets
+  constexpr int LDS = TAPB + KS * ROWS * 64;
+  static_assert(CIN % 16 == 0 && LDS <= 160 * 1024, "dwpw: LDS");
   __shared__ __attribute__((aligned(16))) char sm[LDS];
-#ifdef MLIC_DP_TRACE
-  __shared__ unsigned long long tr[512];
-#endif
-  float* sin = reinterpret_cast<float*>(sm);
-  char* sw = sm + 2 * DP_PSZ * 4;
-  float* sdw = reinterpret_cast<float*>(sw + 2 * WSZ);
-  float* sbias = sdw + CIN * DP_DWP;
+  float* sdw = reinterpret_cast<float*>(sm);
+  float* sbias = sdw + CIN * DR_DWP;
+  char* sa = sm + TAPB;
 
   const int tid = threadIdx.x;
-  for (int i = tid; i < CIN * DP_DWP; i += DP_THREADS) {
-    const int c = i / DP_DWP, k = i - c * DP_DWP;
+  {  // prologue: every weight load in flight before the first LDS store (one memory latency)
+    constexpr int NG = KS * ROWS * 4;  // 16-byte granules of the A image
+    constexpr int NIT = (NG + DR_THREADS - 1) / DR_THREADS;
+    u32x4 st[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int id = tid + it * DR_THREADS;
+      const int q = id & 3, row = (id >> 2) % ROWS, j = (id >> 2) / ROWS;
+      st[it] = u32x4{0u, 0u, 0u, 0u};
+      if (id < NG && row < P.Cout)
+        st[it] = *reinterpret_cast<const u32x4*>((q < 2 ? wh : wl) + (int64_t)row * cin_pad + 16 * j + 8 * (q & 1));
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int id = tid + it * DR_THREADS;
+      const int q = id & 3, row = (id >> 2) % ROWS, j = (id >> 2) / ROWS;
+      if (id < NG) *reinterpret_cast<u32x4*>(sa + (j * ROWS + row) * 64 + ((q ^ dr_swz(row)) << 4)) = st[it];
+    }
+  }
+  for (int i = tid; i < CIN * DR_DWP; i += DR_THREADS) {
+    const int c = i / DR_DWP, k = i - c * DR_DWP;
     sdw[i] = k < 9 ? dww[c * 9 + k] : (k == 9 && dwb ? dwb[c] : 0.0f);
   }
-  for (int r = tid; r < ROWS; r += DP_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
+  for (int r = tid; r < ROWS; r += DR_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
+  __syncthreads();  // the only barrier
 
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, h = lane >> 5;
   const int H = P.H, W = P.W, HW = H * W;
-  const int nseg = (W + DP_TW - 1) / DP_TW;
-  const int nyb = (H + DP_WAVES - 1) / DP_WAVES;
-  const int nblk = nseg * nyb * P.B;
-  if ((int)blockIdx.x >= nblk) return;  // before any barrier: the whole workgroup leaves
-  const int nmine = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int G = nmine * KS;  // k-steps of this workgroup
+  // workgroup tile = DR_WAVES rows x 32 columns (wave w: row y0 + w), so a row's three readers are
+  // waves of one CU, reading it while its lines are in that CU's L1; tiles ordered (image, row
+  // block, segment) and dealt XCD-aware (a multiple of 8 workgroups: blocks b and b + 8 share an XCD
+  // under round-robin placement, speed only): one XCD takes a contiguous run of tiles, so the
+  // horizontal neighbours' edge lines and the next row block's halo rows are L2 neighbours
+  const int nseg = (W + 31) >> 5;
+  const int nyb = (H + DR_WAVES - 1) / DR_WAVES;
+  const int tpi = nseg * nyb;  // workgroup tiles per image
+  const int ntiles = tpi * P.B;
+  const int xcd = (int)blockIdx.x & 7, nslot = (int)gridDim.x >> 3;
+  const int t_end = (int)((int64_t)(xcd + 1) * ntiles / 8);
+  const int tstride = nslot;
+  int tile = (int)((int64_t)xcd * ntiles / 8) + ((int)blockIdx.x >> 3);
+  if (tile >= t_end) return;  // the whole workgroup: no barrier follows
+
   const uint32_t hw4 = (uint32_t)HW * 4u;
   const uint32_t img_bytes = (uint32_t)CIN * hw4;
+  const float* xbase = P.seg[0].p;
+  const int64_t xbs = P.seg[0].bs;
+  const int xe_d = (l32 & 15) == 0 ? -1 : ((l32 & 15) == 15 ? 1 : 0);  // the edge lanes' neighbour
 
-  auto block_of = [&](int n, int& b, int& y0, int& x0) {
-    const int t = (int)blockIdx.x + n * (int)gridDim.x;
-    b = t / (nseg * nyb);
-    const int r = t - b * nseg * nyb;
+  // per segment: 3 main + 3 edge byte offsets (the lane half's channel 8h folded in)
+  struct Seg {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t vm[3], ve[3];
+  };
+  auto seg_of = [&](int t) {
+    Seg s;
+    const int b = t / tpi;
+    const int r = t - b * tpi;
     const int yb = r / nseg;
-    y0 = yb * DP_WAVES;
-    x0 = (r - yb * nseg) * DP_TW;
-  };
-
-  // ---- staging cursor (loads run 2 k-steps ahead of the compute, across block boundaries): thread
-  // t < DP_CH owns patch position t (row t / DP_PC, column t % DP_PC) for all DP_KC channels
-  float rin[DP_KC];
-  u32x4 rw[NWL];
-  uint32_t vpos = DP_OOB;  // byte offset of this thread's patch position in the load block's image
-  __amdgpu_buffer_rsrc_t rs_in = dp_rsrc(P.seg[0].p, img_bytes);
-  auto set_block = [&](int n) {
-    int b, y0, x0;
-    block_of(n, b, y0, x0);
-    rs_in = dp_rsrc(P.seg[0].p + (int64_t)b * P.seg[0].bs, img_bytes);
-    const int r = tid / DP_PC, c = tid - r * DP_PC;
-    const int gy = y0 - 1 + r, gx = x0 - 1 + c;
-    vpos = (tid < DP_CH && gy >= 0 && gy < H && gx >= 0 && gx < W) ? (uint32_t)(gy * W + gx) * 4u : DP_OOB;
-  };
-  auto gload = [&](int g) {
-    const int n = g / KS, k = g - n * KS;
-    if (k == 0) set_block(n);
-    if (tid < DP_CH) {
-      uint32_t so = (uint32_t)(DP_KC * k) * hw4;
-      dp_opaque(so);
+    const int y = yb * DR_WAVES + wave;  // rows past the image read 0 and store nothing
+    const int x = ((r - yb * nseg) << 5) + l32, xe = x + xe_d;
+    s.rs = dr_rsrc(xbase + (int64_t)b * xbs, img_bytes);
+    const uint32_t ch = (uint32_t)(8 * h) * hw4;
 #pragma unroll
-      for (int q = 0; q < DP_KC; ++q) {
-        rin[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_in, vpos, so, 0));
-        so += hw4;
-        dp_opaque(so);
-      }
+    for (int dy = 0; dy < 3; ++dy) {
+      const int yy = y + dy - 1;
+      const bool ok = yy >= 0 && yy < H;
+      s.vm[dy] = ok && x < W ? (uint32_t)(yy * W + x) * 4u + ch : DR_OOB;
+      s.ve[dy] = ok && xe >= 0 && xe < W ? (uint32_t)(yy * W + xe) * 4u + ch : DR_OOB;
     }
-#pragma unroll
-    for (int q = 0; q < NWL; ++q) {
-      const int c = tid + q * DP_THREADS;
-      if (NWQ % DP_THREADS == 0 || c < NWQ) {
-        const int row = c >> 3, g8 = c & 7;
-        const _Float16* src = (g8 < 4 ? wh : wl) + (int64_t)min(row, P.Cout - 1) * cin_pad + DP_KC * k + 8 * (g8 & 3);
-        rw[q] = *reinterpret_cast<const u32x4*>(src);
-      }
-    }
+    return s;
   };
-  auto lstore = [&](int g) {
-    if (tid < DP_CH) {
-      float* pin = sin + (g & 1) * DP_PSZ + tid;
+  // a unit = 4 channel slots of a k-step (half of the lane's 8): main + edge loads of 3 rows each
+  // (24 loads); units are loaded 2 ahead (one k-step), so at most 48 loads are outstanding per wave
+  // (the vmcnt counter holds 63) and each unit waits for exactly its own loads
+  auto load_unit = [&](float (&r)[4][3], float (&e)[4][3], const Seg& s, uint32_t so) {
 #pragma unroll
-      for (int q = 0; q < DP_KC; ++q) pin[q * DP_CH] = rin[q];
-    }
-    char* pw = sw + (g & 1) * WSZ;
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int q = 0; q < NWL; ++q) {
-      const int c = tid + q * DP_THREADS;
-      if (NWQ % DP_THREADS == 0 || c < NWQ) {
-        const int row = c >> 3, g8 = c & 7;
-        *reinterpret_cast<u32x4*>(pw + row * 128 + ((g8 ^ dp_swz(row)) << 4)) = rw[q];
+      for (int dy = 0; dy < 3; ++dy) {
+        r[i][dy] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.rs, s.vm[dy], so, 0));
+        e[i][dy] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.rs, s.ve[dy], so, 0));
       }
+      so += hw4;
+      dr_opaque(so);
     }
   };
 
-  gload(0);
-  lstore(0);
-  if (G > 1) gload(1);
+  float rm[2][4][3], re[2][4][3];  // ring: unit u in slot u & 1
+  Seg cur = seg_of(tile);
+  int nt = tile + tstride < t_end ? tile + tstride : tile;
+  Seg nxt = seg_of(nt);
+  load_unit(rm[0], re[0], cur, 0);
+  load_unit(rm[1], re[1], cur, 4 * hw4);
 
-  const float4* sdw4 = reinterpret_cast<const float4*>(sdw + (8 * h) * DP_DWP);  // this half's channels
-  const int swz = dp_swz(l32);  // rows 32c + l32 share the swizzle of l32
+  const int swz = dr_swz(l32);  // rows 32c + l32 share the swizzle of l32
+  const int gh = (h ^ swz) << 4, gl = ((2 + h) ^ swz) << 4;
   bool bad = false;
-  for (int n = 0; n < nmine; ++n) {
-  floatx16 acc[CT];
+  for (;;) {
+    floatx16 acc[CT];
 #pragma unroll
-  for (int c = 0; c < CT; ++c)
+    for (int c = 0; c < CT; ++c)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
-#pragma unroll 1
-  for (int k = 0; k < KS; ++k) {
-    const int g = n * KS + k;
-    DP_TR(8 * g + 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // step g's slot complete; step g-1's reads of the other slot done
-    asm volatile("" ::: "memory");
-    DP_TR(8 * g + 1);
-    if (g + 1 < G) lstore(g + 1);
-    DP_TR(8 * g + 2);
-    if (g + 2 < G) gload(g + 2);
-    DP_TR(8 * g + 3);
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      // depthwise 3x3 of channels 32k + 16sub + 8h + i at (row y0 + wave, column x0 + l32)
-      const float* pin = sin + (g & 1) * DP_PSZ + (16 * sub + 8 * h) * DP_CH + wave * DP_PC + l32;
+      for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
+
+#pragma unroll 2
+    for (int j = 0; j < KS; ++j) {
+      // the next k-step's loads: this segment's j + 1, or the next segment's k-step 0
+      const bool last = j + 1 == KS;
+      const Seg& ns = last ? nxt : cur;
+      const uint32_t so_next = last ? 0u : (uint32_t)(16 * (j + 1)) * hw4;
       half8 bh, bl;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4* wq = sdw4 + (DP_KC * k + 16 * sub + i) * 3;
-        const float4 w0 = wq[0], w1 = wq[1], w2 = wq[2];
-        const float tw[10] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y};
-        const float* pc = pin + i * DP_CH;
-        float a = 0.0f;
+      for (int u = 0; u < 2; ++u) {
+        // depthwise 3x3 of the lane's channels 16j + 8h + 4u + i at its pixel, split hi / lo
+        const float* tq0 = sdw + (16 * j + 8 * h + 4 * u) * DR_DWP;
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
+        for (int i = 0; i < 4; ++i) {
+          const float4* tq = reinterpret_cast<const float4*>(tq0 + i * DR_DWP);
+          const float4 w0 = tq[0], w1 = tq[1];
+          const float2 w2 = *reinterpret_cast<const float2*>(tq + 2);  // ds_read_b128 x 2 + b64
+          const float tw[10] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y};
+          float a = 0.0f;
 #pragma unroll
-          for (int dx = 0; dx < 3; ++dx) a = fmaf(tw[3 * dy + dx], pc[dy * DP_PC + dx], a);
-        const float v = a + tw[9];
-        const _Float16 hv = (_Float16)v;
-        bh[i] = hv;
-        bl[i] = (_Float16)(v - (float)hv);
+          for (int dy = 0; dy < 3; ++dy) {
+            const float m = rm[u][i][dy], e = re[u][i][dy];
+            a = fmaf(tw[3 * dy + 0], dpp_nb<DPP_ROW_SHR1>(e, m), a);
+            a = fmaf(tw[3 * dy + 1], m, a);
+            a = fmaf(tw[3 * dy + 2], dpp_nb<DPP_ROW_SHL1>(e, m), a);
+          }
+          const float v = a + tw[9];
+          const _Float16 hv = (_Float16)v;
+          bh[4 * u + i] = hv;
+          bl[4 * u + i] = (_Float16)(v - (float)hv);
+        }
+        uint32_t so = so_next + (uint32_t)(4 * u) * hw4;
+        dr_opaque(so);
+        load_unit(rm[u], re[u], ns, so);
       }
-      const int gh = (2 * sub + h) ^ swz, gl = (4 + 2 * sub + h) ^ swz;  // A-fragment granules
-      const char* pw = sw + (g & 1) * WSZ + l32 * 128;
+      __builtin_amdgcn_sched_barrier(0);  // keep the refills behind the depthwise math, ahead of the MFMAs
+      const char* ab = sa + (j * ROWS + l32) * 64;
 #pragma unroll
       for (int c = 0; c < CT; c += 2) {
         const int c1 = (c + 1 < CT) ? c + 1 : c;
-        const half8 ah0 = *reinterpret_cast<const half8*>(pw + c * 32 * 128 + (gh << 4));
-        const half8 al0 = *reinterpret_cast<const half8*>(pw + c * 32 * 128 + (gl << 4));
-        const half8 ah1 = *reinterpret_cast<const half8*>(pw + c1 * 32 * 128 + (gh << 4));
-        const half8 al1 = *reinterpret_cast<const half8*>(pw + c1 * 32 * 128 + (gl << 4));
+        const half8 ah0 = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gh);
+        const half8 al0 = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gl);
+        const half8 ah1 = *reinterpret_cast<const half8*>(ab + c1 * 32 * 64 + gh);
+        const half8 al1 = *reinterpret_cast<const half8*>(ab + c1 * 32 * 64 + gl);
         acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al0, bh, acc[c], 0, 0, 0);
         if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al1, bh, acc[c1], 0, 0, 0);
         acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bl, acc[c], 0, 0, 0);
@@ -227,61 +234,69 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
         if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bh, acc[c1], 0, 0, 0);
       }
     }
-  }
 
-    DP_TR(8 * (n * KS + KS - 1) + 4);
-    // epilogue (pw_resident's): bias, range guard, GELU, residual, one row of 32 columns per wave
-    int b, y0, x0;
-    block_of(n, b, y0, x0);
-    const int y = y0 + wave, x = x0 + l32;
-    if (y >= H || x >= W) continue;
-    const uint32_t cs4 = (uint32_t)P.out_cs * 4u;
-    const uint32_t vo_out = (uint32_t)(y * W + x) * 4u + (uint32_t)(4 * h) * cs4;
-    const auto rs_out = dp_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
-    const auto rs_res = dp_rsrc(RES ? P.res + (int64_t)b * P.res_bs : P.out, RES ? (uint32_t)P.Cout * cs4 : 0u);
-    const float* sb = sbias + 4 * h;
-    const int wexp = P.wexp;
-    uint32_t so_o = 0;
+    // epilogue (pw_resident's): bias, range guard, GELU, residual; one segment of 32 columns
+    {
+      const int b = tile / tpi;
+      const int r = tile - b * tpi;
+      const int yb = r / nseg;
+      const int y = yb * DR_WAVES + wave;
+      const int x = ((r - yb * nseg) << 5) + l32;
+      if (x < W && y < H) {
+        const uint32_t cs4 = (uint32_t)P.out_cs * 4u;
+        const uint32_t vo_out = (uint32_t)(y * W + x) * 4u + (uint32_t)(4 * h) * cs4;
+        const auto rs_out = dr_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
+        const auto rs_res = dr_rsrc(RES ? P.res + (int64_t)b * P.res_bs : P.out, RES ? (uint32_t)P.Cout * cs4 : 0u);
+        const float* sb = sbias + 4 * h;
+        const int wexp = P.wexp;
+        uint32_t so_o = 0;
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      float xr[16];
-      uint32_t oo = so_o;
+        for (int c = 0; c < CT; ++c) {
+          float xr[16];
+          uint32_t oo = so_o;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (r > 0) {
-          oo += (((r & 3) == 0) ? 5u : 1u) * cs4;  // co_u = 32c + (r&3) + 8(r>>2)
-          dp_opaque(oo);
+          for (int q = 0; q < 16; ++q) {
+            if (q > 0) {
+              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;  // co_u = 32c + (q&3) + 8(q>>2)
+              dr_opaque(oo);
+            }
+            xr[q] = RES ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, vo_out, oo, 0)) : 0.0f;
+          }
+          float4 bq[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) bq[g] = *reinterpret_cast<const float4*>(sb + c * 32 + 8 * g);
+          oo = so_o;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int co = c * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+            if (q > 0) {
+              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;
+              dr_opaque(oo);
+            }
+            const float4 b4 = bq[q >> 2];
+            const float bv = (q & 3) == 0 ? b4.x : (q & 3) == 1 ? b4.y : (q & 3) == 2 ? b4.z : b4.w;
+            float v = ldexpf(acc[c][q], -wexp) + bv;
+            bad |= !(fabsf(v) <= 3.4e38f);
+            if (GELU) v = gelu_erf(v);
+            v += xr[q];
+            if (c * 32 + 32 <= P.Cout || co < P.Cout)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
+          }
+          so_o += 32 * cs4;
+          dr_opaque(so_o);
         }
-        xr[r] = RES ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, vo_out, oo, 0)) : 0.0f;
       }
-      oo = so_o;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = c * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (r > 0) {
-          oo += (((r & 3) == 0) ? 5u : 1u) * cs4;
-          dp_opaque(oo);
-        }
-        float v = ldexpf(acc[c][r], -wexp);
-        v += sb[c * 32 + (r & 3) + 8 * (r >> 2)];
-        bad |= !(fabsf(v) <= 3.4e38f);
-        if (GELU) v = gelu_erf(v);
-        v += xr[r];
-        if (c * 32 + 32 <= P.Cout || co < P.Cout)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
-      }
-      so_o += 32 * cs4;
-      dp_opaque(so_o);
     }
+    if (nt == tile) break;
+    tile = nt;
+    cur = nxt;
+    nt = tile + tstride < t_end ? tile + tstride : tile;
+    nxt = seg_of(nt);
   }
   range_report(P.rflag, bad);
-#ifdef MLIC_DP_TRACE
-  if (blockIdx.x == 0 && tid == 0)
-    for (int i = 0; i < 512; ++i) g_dp_trace[i] = tr[i];
-#endif
 }
 
-static int dp_num_cus() {
+static int dr_num_cus() {
   static int n = 0;
   if (n == 0) {
     int dev = 0;
@@ -291,25 +306,33 @@ static int dp_num_cus() {
   return n;
 }
 
+// (CIN, CT) instantiated: Cin = Cout = N of g_a / g_s (MLICPP_L 192, M 160, S2 128, S 96, and the
+// small-decoder model's N / 4 = 48)
+#define DR_SHAPES(X) X(192, 6) X(160, 5) X(128, 4) X(96, 3) X(48, 2)
+
 bool dwpw_ok(const ConvParams& P, int cin_pad) {
-  if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad != P.Cin) return false;
+  if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.epi & ~(EPI_GELU | EPI_RES)) return false;
   if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W) return false;
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
   const int ct = (P.Cout + 31) / 32;
-  return (P.Cin == 192 && ct == 6) || (P.Cin == 128 && ct == 4) || (P.Cin == 96 && ct == 3) ||
-         (P.Cin == 160 && ct == 5);
+#define DR_OK(CIN, CT) \
+  if (P.Cin == CIN && ct == CT) return true;
+  DR_SHAPES(DR_OK)
+#undef DR_OK
+  return false;
 }
 
 template <int CIN, int CT>
 static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                         const float* dwb, hipStream_t st) {
-  const int64_t nblk = (int64_t)((P.W + DP_TW - 1) / DP_TW) * ((P.H + DP_WAVES - 1) / DP_WAVES) * P.B;
-  const dim3 grid((unsigned)std::min<int64_t>(nblk, (int64_t)dp_num_cus()));
+  const int64_t want = (int64_t)((P.W + 31) / 32) * ((P.H + DR_WAVES - 1) / DR_WAVES) * P.B;  // workgroup tiles
+  const int64_t g = std::min<int64_t>(want, (int64_t)dr_num_cus());
+  const dim3 grid((unsigned)((g + 7) / 8 * 8));  // a multiple of 8: the XCD-aware deal
   const bool gelu = (P.epi & EPI_GELU) != 0, res = (P.epi & EPI_RES) != 0;
 #define MLIC_DP(G, R) \
-  hipLaunchKernelGGL((dwpw_kernel<CIN, CT, G, R>), grid, dim3(DP_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
+  hipLaunchKernelGGL((dwpw_kernel<CIN, CT, G, R>), grid, dim3(DR_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
   if (gelu && res) MLIC_DP(true, true);
   else if (gelu) MLIC_DP(true, false);
   else if (res) MLIC_DP(false, true);
@@ -321,12 +344,13 @@ static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16*
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st) {
   MLIC_CHECK(dwpw_ok(P, cin_pad) && dww, "dwpw: unsupported shape");
-  switch (P.Cin) {
-    case 192: launch_dwpw<192, 6>(P, wh, wl, cin_pad, dww, dwb, st); break;
-    case 160: launch_dwpw<160, 5>(P, wh, wl, cin_pad, dww, dwb, st); break;
-    case 128: launch_dwpw<128, 4>(P, wh, wl, cin_pad, dww, dwb, st); break;
-    default: launch_dwpw<96, 3>(P, wh, wl, cin_pad, dww, dwb, st); break;
+#define DR_RUN(CIN, CT)                                         \
+  if (P.Cin == CIN) {                                           \
+    launch_dwpw<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st);     \
+    return;                                                     \
   }
+  DR_SHAPES(DR_RUN)
+#undef DR_RUN
 }
 
 }  // namespace mlic

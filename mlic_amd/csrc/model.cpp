@@ -432,11 +432,8 @@ bool Model::hoist_on() const {
   return on && chain_on() && hoist_.Cout > 0;
 }
 
-// $MLIC_DWPW=1: the fused depthwise+pointwise kernel (conv_dwpw.hip) for the stride-1 dwsep convs.
-// Off by default: measured slower than depthwise + resident pointwise on MI355X (g_a stage 1,
-// 8 x 192 x 544 x 960: 3.5 ms fused vs 1.29 + 1.77 ms; its per-k-step barrier keeps the whole
-// workgroup's store-issue-bound epilogue and VMEM-issue-bound staging from overlapping the MFMAs,
-// DESIGN.md).  Kept as the bit-exact reference point for the next design.
+// $MLIC_DWPW=1: the fused dwpw kernel (conv_dwpw.hip) instead of depthwise + resident pointwise for
+// the stride-1 dwsep convs (A/B switch; the results are bit-identical)
 bool Model::dwpw_on() const {
   static const bool on = [] {
     const char* e = std::getenv("MLIC_DWPW");

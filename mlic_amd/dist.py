@@ -40,6 +40,27 @@ def lpt_shard(sizes: Sequence[Tuple[int, int]], world: int) -> List[List[int]]:
     return out
 
 
+def group_shard(keys: Sequence, sizes: Sequence[Tuple[int, int]], world: int) -> List[List[int]]:
+    """Contiguous partition of the jobs, ordered by their batch key (weight set, shape), into `world`
+    slices of near-equal padded pixel count (each within one job's weight of its share).  A rank then
+    runs a few whole batches instead of the one or two images of every (weights, shape) group that
+    LPT deals it round-robin (BASELINE config 4: 144 equal jobs in 12 groups -> 18 jobs in <= 3
+    batches per rank at world 8).  Deterministic."""
+    order = sorted(range(len(keys)), key=lambda i: (keys[i], i))
+    w = [padded_pixels(*sizes[i]) for i in order]
+    total = float(sum(w))
+    out: List[List[int]] = [[] for _ in range(world)]
+    acc, r = 0.0, 0
+    for i, wi in zip(order, w):
+        while r < world - 1 and acc + 0.5 * wi > total * (r + 1) / world:
+            r += 1
+        out[r].append(i)
+        acc += wi
+    for s in out:
+        s.sort()
+    return out
+
+
 def gather_records(local: torch.Tensor, max_per_rank: int) -> torch.Tensor:
     """all_gather fixed-size [max_per_rank, RECORD_LEN] float64 blocks (rows with job = -1 are
     padding) and return the valid rows sorted by job id.  Works single-process too."""

@@ -252,8 +252,10 @@ class MLICPlusPlus(nn.Module):
     @torch.no_grad()
     def compress(self, x: torch.Tensor, **kw):
         """mlicpp.py:199-290.  strings = [[y_stream per image], [z_stream per image]] (B = 1: exactly
-        the reference's layout; for B > 1 each image gets its own y stream instead of one shared one)."""
-        torch.cuda.synchronize(x.device)
+        the reference's layout; for B > 1 each image gets its own y stream instead of one shared one).
+        cost_time brackets the call with the caller's stream synchronised (the reference synchronises the
+        whole device, mlicpp.py:200, 282; a stream keeps concurrent callers on other streams apart)."""
+        torch.cuda.current_stream(x.device).synchronize()
         t0 = time.time()
         B, _, H, W = x.shape
         if H % 64 or W % 64:
@@ -272,14 +274,14 @@ class MLICPlusPlus(nn.Module):
             _lib.call("mlic_encoded_copy", h, b, yb, zb)
             ys.append(C.string_at(yb, yl.value))
             zs.append(C.string_at(zb, zl.value))
-        torch.cuda.synchronize(x.device)
+        torch.cuda.current_stream(x.device).synchronize()
         return {"strings": [ys, zs], "shape": torch.Size([H // 64, W // 64]), "cost_time": time.time() - t0}
 
     @torch.no_grad()
     def decompress(self, strings, shape, **kw):
         """mlicpp.py:292-378."""
         dev = self.device
-        torch.cuda.synchronize(dev)
+        torch.cuda.current_stream(dev).synchronize()
         t0 = time.time()
         ys, zs = list(strings[0]), list(strings[1])
         B = len(zs)
@@ -298,7 +300,7 @@ class MLICPlusPlus(nn.Module):
         sc = self._vbr_scales(B, **kw)
         _lib.call("mlic_decompress_v", h, self._stream(), yp, yl, zp, zl, B, hz, wz, x_hat.data_ptr(),
                   sc.ctypes.data)
-        torch.cuda.synchronize(dev)
+        torch.cuda.current_stream(dev).synchronize()
         return {"x_hat": x_hat, "cost_time": time.time() - t0}
 
     def encoded_streams(self, b: int = 0):

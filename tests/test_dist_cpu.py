@@ -18,6 +18,26 @@ def test_lpt_shard_balances_and_covers():
     assert mdist.lpt_shard(sizes, 4) == shards  # deterministic
 
 
+def test_group_shard_whole_batches():
+    """BASELINE config 4 at 8 ranks: 144 equal jobs in 12 (weight set, shape) groups -> 18 jobs per
+    rank in at most 3 batches (LPT would deal every rank 1-3 images of up to 12 groups)."""
+    keys = [(r, H, W) for r in range(6) for (H, W) in [(512, 768)] * 20 + [(768, 512)] * 4]
+    sizes = [(k[1], k[2]) for k in keys]
+    for world in (1, 2, 3, 4, 8):
+        shards = mdist.group_shard(keys, sizes, world)
+        assert sorted(i for s in shards for i in s) == list(range(len(keys)))
+        counts = [len(s) for s in shards]
+        assert max(counts) - min(counts) <= 1, counts
+        assert all(len({keys[i] for i in s}) <= -(-12 // world) + 2 for s in shards)
+        if world == 8:
+            assert all(len({keys[i] for i in s}) <= 3 for s in shards)
+        assert mdist.group_shard(keys, sizes, world) == shards
+    mixed = [(2176, 3840)] * 2 + [(1088, 1920)] * 6
+    shards = mdist.group_shard([s for s in mixed], mixed, 2)
+    loads = [sum(mdist.padded_pixels(*mixed[i]) for i in s) for s in shards]
+    assert max(loads) - min(loads) <= mdist.padded_pixels(2176, 3840)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -89,7 +109,8 @@ def _sweep_worker(rank, world, port, q):
 
 def test_kodak_sweep_sharded_world2():
     """BASELINE config 4's job list (24 Kodak-size images incl. 4 portrait x 6 lambda stand-ins = 144
-    jobs) sharded by bench.py over 2 ranks with LPT; the gathered records are complete and sorted."""
+    jobs) sharded by bench.py over 2 ranks in whole (weight set, shape) batches; the gathered records are
+    complete and sorted."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -104,7 +125,8 @@ def test_kodak_sweep_sharded_world2():
     rows = next(g[0] for g in got if g[0] is not None)
     assert all(g[1] == 144 for g in got)
     counts = sorted(g[2][0] for g in got)
-    assert sum(counts) == 144 and counts[1] - counts[0] <= 4  # LPT by pixels: balanced to one job's worth
+    assert sum(counts) == 144 and counts[1] - counts[0] <= 1  # equal-pixel jobs: balanced to one job
+    assert all(g[3] <= 7 for g in got)  # each rank runs a few whole batches
     assert [int(r[0]) for r in rows] == list(range(144))
     for r in rows:
         j = int(r[0])

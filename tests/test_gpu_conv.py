@@ -267,10 +267,15 @@ def test_depthwise(shape):
 
 
 @pytest.mark.parametrize("B,Cn,H,W,epi", [
-    (2, 192, 40, 100, 1),    # GELU; 100 columns = 3 segments of 30 + a ragged one
-    (1, 192, 17, 61, 0),     # odd sizes, last row block partial
+    (2, 192, 40, 100, 1),    # GELU; 100 columns = 3 segments of 32 + a ragged 4
+    (1, 192, 17, 61, 0),     # odd sizes, ragged last segment
     (2, 192, 68, 120, 1 | 64),  # latent grid, GELU + residual
-    (1, 128, 24, 30, 0),     # Cin 128, one exact segment
+    (1, 128, 24, 30, 0),     # Cin 128, one ragged segment
+    (3, 192, 20, 96, 64),    # residual only, exact 32-column segments
+    (2, 160, 9, 64, 1),      # MLICPP_M width
+    (2, 96, 33, 70, 1 | 64), # MLICPP_S width
+    (2, 48, 16, 160, 1 | 64),  # the small-decoder model's g_s width (3 k-steps)
+    (1, 192, 1, 33, 1),      # a single row: both vertical taps out of the image
 ])
 def test_dwpw_fused(B, Cn, H, W, epi):
     """Fused depthwise 3x3 + pointwise 1x1 (conv_dwpw.hip) == depthwise kernel then the resident-weight
