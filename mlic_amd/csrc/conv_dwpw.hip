@@ -34,6 +34,7 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int DR_WAVES = 8;
 constexpr int DR_THREADS = DR_WAVES * 64;
@@ -296,6 +297,259 @@ __global__ __launch_bounds__(DR_THREADS) void dwpw_kernel(ConvParams P, const _F
   range_report(P.rflag, bad);
 }
 
+// -------------------------------------------------------------------------------------------------
+// Pixel-pair form (default).  Same LDS-resident weights and depthwise order as dwpw_kernel above,
+// but every lane owns TWO adjacent pixels of one row: its activation loads are dwordx2 (8 B per lane
+// per channel and row: a quarter of dwpw_kernel's vector-memory instructions per pixel, whose main +
+// edge b32 loads were its issue limit), and the two pixels are the columns of two MFMA B fragments
+// (e = 0, 1: column n <-> pixel xl + e), whose accumulators hold, lane for lane, the same output
+// channel of both pixels -- the epilogue stores them as dwordx2 too.
+// A wave row segment is 64 loaded columns (lane n: xl = x0 - 2 + 2n) for 60 output columns: lanes
+// 0 and 31 of each lane half only supply the halo (x0 - 1 via lane 0's second pixel, x0 + 60 via lane
+// 31's first) and store nothing, so the horizontal neighbours are plain DPP wave shifts with no edge
+// loads (the neighbour a halo lane receives across the lane-half seam is never used).  MFMA columns
+// wasted: 2 of 32.  One wave per SIMD (4 waves, 256 threads, one workgroup per CU): the two-pixel
+// accumulators of all Cout rows (CT x 2 x 16 registers) live beside a two-k-step load ring.
+// Workgroup tile = 4 rows x 60 columns (wave w: row y0 + w), dealt XCD-aware as dwpw_kernel's.
+// Needs W even (a lane's pixel pair is either inside the row or entirely outside it) and an even
+// number of 16-channel k-steps (the ring's slot of a k-step is static across tiles).
+constexpr int DP_WAVES = 4;
+constexpr int DP_THREADS = DP_WAVES * 64;
+constexpr int DP_SEG = 60;
+constexpr int DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138;
+
+namespace {
+typedef float float2v __attribute__((ext_vector_type(2)));
+// lane - 1 (SHR) / lane + 1 (SHL) of the whole wave; lane 0 / 63 receive 0 (never used)
+template <int CTRL>
+__device__ __forceinline__ float wave_nb(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+}  // namespace
+
+template <int CIN, int CT, bool GELU, bool RES>
+__global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _Float16* __restrict__ wh,
+                                                         const _Float16* __restrict__ wl, int cin_pad,
+                                                         const float* __restrict__ dww, const float* __restrict__ dwb) {
+  constexpr int KS = CIN / 16;
+  constexpr int ROWS = CT * 32;
+  constexpr int TAPB = CIN * DR_DWP * 4 + ROWS * 4;
+  constexpr int LDS = TAPB + KS * ROWS * 64;
+  static_assert(CIN % 32 == 0 && LDS <= 160 * 1024, "dwpw2: LDS / even k-steps");
+  __shared__ __attribute__((aligned(16))) char sm[LDS];
+  float* sdw = reinterpret_cast<float*>(sm);
+  float* sbias = sdw + CIN * DR_DWP;
+  char* sa = sm + TAPB;
+
+  const int tid = threadIdx.x;
+  {  // prologue: the A image (dwpw_kernel's layout), every load in flight before the first store
+    constexpr int NG = KS * ROWS * 4;
+    constexpr int NIT = (NG + DP_THREADS - 1) / DP_THREADS;
+    u32x4 st[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int id = tid + it * DP_THREADS;
+      const int q = id & 3, row = (id >> 2) % ROWS, j = (id >> 2) / ROWS;
+      st[it] = u32x4{0u, 0u, 0u, 0u};
+      if (id < NG && row < P.Cout)
+        st[it] = *reinterpret_cast<const u32x4*>((q < 2 ? wh : wl) + (int64_t)row * cin_pad + 16 * j + 8 * (q & 1));
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int id = tid + it * DP_THREADS;
+      const int q = id & 3, row = (id >> 2) % ROWS, j = (id >> 2) / ROWS;
+      if (id < NG) *reinterpret_cast<u32x4*>(sa + (j * ROWS + row) * 64 + ((q ^ dr_swz(row)) << 4)) = st[it];
+    }
+  }
+  for (int i = tid; i < CIN * DR_DWP; i += DP_THREADS) {
+    const int c = i / DR_DWP, k = i - c * DR_DWP;
+    sdw[i] = k < 9 ? dww[c * 9 + k] : (k == 9 && dwb ? dwb[c] : 0.0f);
+  }
+  for (int r = tid; r < ROWS; r += DP_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
+  __syncthreads();  // the only barrier
+
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 31, h = lane >> 5;
+  const int H = P.H, W = P.W, HW = H * W;
+  const int nseg = (W + DP_SEG - 1) / DP_SEG;
+  const int nyb = (H + DP_WAVES - 1) / DP_WAVES;
+  const int tpi = nseg * nyb;
+  const int ntiles = tpi * P.B;
+  const int xcd = (int)blockIdx.x & 7, nslot = (int)gridDim.x >> 3;
+  const int t_end = (int)((int64_t)(xcd + 1) * ntiles / 8);
+  int tile = (int)((int64_t)xcd * ntiles / 8) + ((int)blockIdx.x >> 3);
+  if (tile >= t_end) return;  // the whole workgroup: no barrier follows
+
+  const uint32_t hw4 = (uint32_t)HW * 4u;
+  const uint32_t img_bytes = (uint32_t)CIN * hw4;
+  const float* xbase = P.seg[0].p;
+  const int64_t xbs = P.seg[0].bs;
+
+  struct Seg2 {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t vo[3];
+  };
+  auto seg_of = [&](int t) {
+    Seg2 s;
+    const int b = t / tpi;
+    const int r = t - b * tpi;
+    const int yb = r / nseg;
+    const int y = yb * DP_WAVES + wave;  // rows past the image read 0 and store nothing
+    const int xl = (r - yb * nseg) * DP_SEG - 2 + 2 * n;
+    s.rs = dr_rsrc(xbase + (int64_t)b * xbs, img_bytes);
+    const uint32_t ch = (uint32_t)(8 * h) * hw4;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int yy = y + dy - 1;
+      s.vo[dy] = yy >= 0 && yy < H && xl >= 0 && xl < W ? (uint32_t)(yy * W + xl) * 4u + ch : DR_OOB;
+    }
+    return s;
+  };
+  // one k-step: the lane's 8 channels x 3 rows as pixel pairs (24 dwordx2 loads)
+  auto load_ks = [&](float2v (&r)[8][3], const Seg2& s, uint32_t so) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+        r[i][dy] = __builtin_bit_cast(float2v, __builtin_amdgcn_raw_buffer_load_b64(s.rs, s.vo[dy], so, 0));
+      so += hw4;
+      dr_opaque(so);
+    }
+  };
+
+  float2v ring[2][8][3];  // k-step j in slot j & 1
+  Seg2 cur = seg_of(tile);
+  int nt = tile + nslot < t_end ? tile + nslot : tile;
+  Seg2 nxt = seg_of(nt);
+  load_ks(ring[0], cur, 0);
+
+  const int swz = dr_swz(n);
+  const int gh = (h ^ swz) << 4, gl = ((2 + h) ^ swz) << 4;
+  bool bad = false;
+  for (;;) {
+    floatx16 acc[CT][2];
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][e][r] = 0.0f;
+
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      // the next k-step's loads (this segment's j + 1, or the next segment's k-step 0) go out first:
+      // their slot was consumed by k-step j - 1
+      if (j + 1 < KS) load_ks(ring[(j + 1) & 1], cur, (uint32_t)(16 * (j + 1)) * hw4);
+      else load_ks(ring[0], nxt, 0u);
+      float2v (&rk)[8][3] = ring[j & 1];
+      half8 bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        // depthwise 3x3 of channel 16j + 8h + i at the lane's two pixels, dw3x3's order
+        const float4* tq = reinterpret_cast<const float4*>(sdw + (16 * j + 8 * h + i) * DR_DWP);
+        const float4 w0 = tq[0], w1 = tq[1];
+        const float2 w2 = *reinterpret_cast<const float2*>(tq + 2);
+        const float tw[10] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y};
+        float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const float p0 = rk[i][dy].x, p1 = rk[i][dy].y;
+          a0 = fmaf(tw[3 * dy + 0], wave_nb<DPP_WAVE_SHR1>(p1), a0);
+          a0 = fmaf(tw[3 * dy + 1], p0, a0);
+          a0 = fmaf(tw[3 * dy + 2], p1, a0);
+          a1 = fmaf(tw[3 * dy + 0], p0, a1);
+          a1 = fmaf(tw[3 * dy + 1], p1, a1);
+          a1 = fmaf(tw[3 * dy + 2], wave_nb<DPP_WAVE_SHL1>(p0), a1);
+        }
+        const float v0 = a0 + tw[9], v1 = a1 + tw[9];
+        const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+        bh[0][i] = h0;
+        bh[1][i] = h1;
+        bl[0][i] = (_Float16)(v0 - (float)h0);
+        bl[1][i] = (_Float16)(v1 - (float)h1);
+      }
+      const char* ab = sa + (j * ROWS + n) * 64;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const half8 ah = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gh);
+        const half8 al = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gl);
+        // pw_resident's term order per accumulator: lo.hi, hi.lo, hi.hi
+        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[0], acc[c][0], 0, 0, 0);
+        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[1], acc[c][1], 0, 0, 0);
+        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[0], acc[c][0], 0, 0, 0);
+        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[1], acc[c][1], 0, 0, 0);
+        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[0], acc[c][0], 0, 0, 0);
+        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[1], acc[c][1], 0, 0, 0);
+      }
+    }
+
+    // epilogue (pw_resident's op sequence): bias, range guard, GELU, residual; pixel pairs as dwordx2
+    {
+      const int b = tile / tpi;
+      const int r = tile - b * tpi;
+      const int yb = r / nseg;
+      const int y = yb * DP_WAVES + wave;
+      const int xl = (r - yb * nseg) * DP_SEG - 2 + 2 * n;
+      if (n >= 1 && n <= 30 && xl < W && y < H) {
+        const uint32_t cs4 = (uint32_t)P.out_cs * 4u;
+        const uint32_t vo_out = (uint32_t)(y * W + xl) * 4u + (uint32_t)(4 * h) * cs4;
+        const auto rs_out = dr_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
+        const auto rs_res = dr_rsrc(RES ? P.res + (int64_t)b * P.res_bs : P.out, RES ? (uint32_t)P.Cout * cs4 : 0u);
+        const float* sb = sbias + 4 * h;
+        const int wexp = P.wexp;
+        uint32_t so_o = 0;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          float2v xr[16];
+          uint32_t oo = so_o;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            if (q > 0) {
+              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;  // co_u = 32c + (q&3) + 8(q>>2)
+              dr_opaque(oo);
+            }
+            xr[q] = RES ? __builtin_bit_cast(float2v, __builtin_amdgcn_raw_buffer_load_b64(rs_res, vo_out, oo, 0))
+                        : float2v{0.0f, 0.0f};
+          }
+          float4 bq[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) bq[g] = *reinterpret_cast<const float4*>(sb + c * 32 + 8 * g);
+          oo = so_o;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int co = c * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+            if (q > 0) {
+              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;
+              dr_opaque(oo);
+            }
+            const float4 b4 = bq[q >> 2];
+            const float bv = (q & 3) == 0 ? b4.x : (q & 3) == 1 ? b4.y : (q & 3) == 2 ? b4.z : b4.w;
+            float2v v;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              float t = ldexpf(acc[c][e][q], -wexp) + bv;
+              bad |= !(fabsf(t) <= 3.4e38f);
+              if (GELU) t = gelu_erf(t);
+              v[e] = t + xr[q][e];
+            }
+            if (c * 32 + 32 <= P.Cout || co < P.Cout)
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs_out, vo_out, oo, 0);
+          }
+          so_o += 32 * cs4;
+          dr_opaque(so_o);
+        }
+      }
+    }
+    if (nt == tile) break;
+    tile = nt;
+    cur = nxt;
+    nt = tile + nslot < t_end ? tile + nslot : tile;
+    nxt = seg_of(nt);
+  }
+  range_report(P.rflag, bad);
+}
+
 static int dr_num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -341,13 +595,49 @@ static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16*
   HIP_OK(hipGetLastError());
 }
 
+template <int CIN, int CT>
+static void launch_dwpw2(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                         const float* dwb, hipStream_t st) {
+  const int64_t want = (int64_t)((P.W + DP_SEG - 1) / DP_SEG) * ((P.H + DP_WAVES - 1) / DP_WAVES) * P.B;
+  const int64_t g = std::min<int64_t>(want, (int64_t)dr_num_cus());
+  const dim3 grid((unsigned)((g + 7) / 8 * 8));
+  const bool gelu = (P.epi & EPI_GELU) != 0, res = (P.epi & EPI_RES) != 0;
+#define MLIC_DP(G, R) \
+  hipLaunchKernelGGL((dwpw2_kernel<CIN, CT, G, R>), grid, dim3(DP_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
+  if (gelu && res) MLIC_DP(true, true);
+  else if (gelu) MLIC_DP(true, false);
+  else if (res) MLIC_DP(false, true);
+  else MLIC_DP(false, false);
+#undef MLIC_DP
+  HIP_OK(hipGetLastError());
+}
+
+// $MLIC_DWPW_V=1: the lane-per-pixel form (A/B only); default the pixel-pair form where it applies
+static int dwpw_version() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("MLIC_DWPW_V");
+    v = (e && e[0] == '1') ? 1 : 2;
+  }
+  return v;
+}
+
+static bool dwpw2_ok(const ConvParams& P) { return (P.W % 2) == 0 && (P.Cin % 32) == 0; }
+
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st) {
   MLIC_CHECK(dwpw_ok(P, cin_pad) && dww, "dwpw: unsupported shape");
-#define DR_RUN(CIN, CT)                                         \
-  if (P.Cin == CIN) {                                           \
-    launch_dwpw<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st);     \
-    return;                                                     \
+  const bool v2 = dwpw_version() == 2 && dwpw2_ok(P);
+#define DR_RUN(CIN, CT)                                              \
+  if (P.Cin == CIN) {                                                \
+    if constexpr (CIN % 32 == 0) {                                   \
+      if (v2) {                                                      \
+        launch_dwpw2<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st);     \
+        return;                                                      \
+      }                                                              \
+    }                                                                \
+    launch_dwpw<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st);          \
+    return;                                                          \
   }
   DR_SHAPES(DR_RUN)
 #undef DR_RUN

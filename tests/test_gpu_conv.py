@@ -276,6 +276,12 @@ def test_depthwise(shape):
     (2, 96, 33, 70, 1 | 64), # MLICPP_S width
     (2, 48, 16, 160, 1 | 64),  # the small-decoder model's g_s width (3 k-steps)
     (1, 192, 1, 33, 1),      # a single row: both vertical taps out of the image
+    # pixel-pair form (even W): 60-column segments, 4-row workgroup tiles
+    (2, 192, 13, 120, 1 | 64),  # two exact segments, ragged row block
+    (1, 192, 6, 62, 0),      # one segment + one pixel pair
+    (1, 96, 3, 2, 1),        # a single pair: both halo pairs out of the image
+    (1, 192, 5, 960, 1),     # full-resolution width
+    (2, 128, 8, 184, 64),    # Cin 128, ragged last segment (4 pairs)
 ])
 def test_dwpw_fused(B, Cn, H, W, epi):
     """Fused depthwise 3x3 + pointwise 1x1 (conv_dwpw.hip) == depthwise kernel then the resident-weight

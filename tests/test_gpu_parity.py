@@ -484,6 +484,65 @@ def test_4k_parity_and_roundtrip():
     assert torch.equal(d["x_hat"], out["x_hat"])
 
 
+@pytest.mark.parametrize("name", ["MLICPP_S", "MLICPP_M_SMALL_DEC"])
+def test_config_size_parity_1080p(name):
+    """BASELINE configs 3 (MLICPP_S) and 3b (MLICPP_M_SMALL_DEC) at their own size, 1920x1088, where
+    the per-image grid selects different kernels than at Kodak size (conv_dispatch.cpp conv_select):
+    bpp / PSNR vs the CPU oracle, x_hat vs the oracle's x_hat >= 60 dB, and the bit-exact round trip
+    (mlicpp_small_decoder.py:86-192 for the small decoder)."""
+    H, W = 1088, 1920
+    x = synthetic.synth_image(H, W, 11)
+    net = rate_net(name, 2)
+    out = net(x.to(DEV))
+    torch.cuda.synchronize()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    o = ref.RefMLIC(name, synthetic.synth_state_dict(name, rate=2)).forward(x)
+    bg, bc = bpp(out, H * W), ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"],
+                                                      o["likelihoods"]["z_likelihoods"], H * W)
+    pg, pc = ref.psnr_uint8(x, out["x_hat"].cpu()), ref.psnr_uint8(x, o["x_hat"])
+    key = f"1080p_{name}_r2"
+    PARITY[key] = {"bpp_gpu": bg, "bpp_cpu": bc, "psnr_gpu": pg, "psnr_cpu": pc,
+                   "xhat_psnr_vs_cpu_db": _psnr_f(out["x_hat"].cpu(), o["x_hat"])}
+    assert abs(bg - bc) <= 1e-3, PARITY[key]
+    assert abs(pg - pc) <= 0.01, PARITY[key]
+    assert PARITY[key]["xhat_psnr_vs_cpu_db"] >= 60.0, PARITY[key]
+    net.update()
+    c = net.compress(x.to(DEV))
+    d = net.decompress(c["strings"], c["shape"])
+    assert torch.equal(d["x_hat"], out["x_hat"])
+
+
+def test_vbr_4k_mixed_levels_vs_oracle_and_per_image():
+    """BASELINE config 5 size with the VBR model (mlicpp_vbr.py:137-519): a 3840x2176 batch with one
+    level per image equals one call per image bit for bit (forward, bitstreams, decoded image), and
+    one image's bpp / PSNR match the CPU oracle at that level."""
+    name, H, W = "MLICPP_L_VBR", 2176, 3840
+    net = rate_net(name, 2)
+    net.update()
+    levels = [1, 4]
+    x = torch.cat([synthetic.synth_image(H, W, 70 + i) for i in range(2)])
+    xd = x.to(DEV)
+    f = net(xd, stage=2, s=levels)
+    c = net.compress(xd, stage=2, s=levels)
+    d = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
+    assert torch.equal(d["x_hat"], f["x_hat"])
+    for i, lv in enumerate(levels):
+        fi = net(xd[i:i + 1], stage=2, s=lv)
+        assert torch.equal(fi["x_hat"], f["x_hat"][i:i + 1])
+        ci = net.compress(xd[i:i + 1], stage=2, s=lv)
+        assert ci["strings"][0][0] == c["strings"][0][i] and ci["strings"][1][0] == c["strings"][1][i]
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    o = ref.RefMLIC(name, synthetic.synth_state_dict(name, rate=2)).forward(x[1:2], s=levels[1])
+    yl, zl = f["likelihoods"]["y_likelihoods"][1:2].cpu(), f["likelihoods"]["z_likelihoods"][1:2].cpu()
+    bg = ref.bpp_from_likelihoods(yl, zl, H * W)
+    bc = ref.bpp_from_likelihoods(o["likelihoods"]["y_likelihoods"], o["likelihoods"]["z_likelihoods"], H * W)
+    pg, pc = ref.psnr_uint8(x[1:2], f["x_hat"][1:2].cpu()), ref.psnr_uint8(x[1:2], o["x_hat"])
+    PARITY["4k_MLICPP_L_VBR_s4"] = {"bpp_gpu": bg, "bpp_cpu": bc, "psnr_gpu": pg, "psnr_cpu": pc,
+                                    "xhat_psnr_vs_cpu_db": _psnr_f(f["x_hat"][1:2].cpu(), o["x_hat"])}
+    assert abs(bg - bc) <= 1e-3, PARITY["4k_MLICPP_L_VBR_s4"]
+    assert abs(pg - pc) <= 0.01, PARITY["4k_MLICPP_L_VBR_s4"]
+
+
 @pytest.mark.parametrize("kind,idx,cin", [("anchor", 0, 640), ("anchor", 5, 832), ("nonanchor", 0, 704),
                                           ("nonanchor", 9, 960)])
 def test_entropy_parameters_chain_vs_oracle(kind, idx, cin):
