@@ -121,6 +121,26 @@ __device__ __forceinline__ float gelu_erf(float x) {
   const float e = __builtin_amdgcn_exp2f(z * (z * -1.44269504088896341f));  // exp(-z^2)
   return __builtin_fmaxf(x, 0.0f) - ax * (q * e);
 }
+// gelu_erf of two values at once: the same operation sequence element for element (bit-identical),
+// with the multiply / FMA steps as packed-fp32 VALU (v_pk_mul_f32 / v_pk_fma_f32: one instruction
+// for both) -- for epilogues that hold pixel pairs
+typedef float mlic_float2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ mlic_float2 gelu_erf2(mlic_float2 x) {
+  const mlic_float2 ax = {__builtin_fabsf(x.x), __builtin_fabsf(x.y)};
+  const mlic_float2 z = ax * 0.70710678118654752440f;
+  const mlic_float2 d = __builtin_elementwise_fma(mlic_float2{0.3275911f, 0.3275911f}, z, mlic_float2{1.0f, 1.0f});
+  const mlic_float2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  mlic_float2 q = __builtin_elementwise_fma(mlic_float2{0.5307027101516724f, 0.5307027101516724f}, t,
+                                            mlic_float2{-0.726576030254364f, -0.726576030254364f});
+  q = __builtin_elementwise_fma(q, t, mlic_float2{0.710706889629364f, 0.710706889629364f});
+  q = __builtin_elementwise_fma(q, t, mlic_float2{-0.14224836230278015f, -0.14224836230278015f});
+  q = __builtin_elementwise_fma(q, t, mlic_float2{0.1274147927761078f, 0.1274147927761078f});
+  q = q * t;
+  const mlic_float2 zz = z * (z * -1.44269504088896341f);
+  const mlic_float2 e = {__builtin_amdgcn_exp2f(zz.x), __builtin_amdgcn_exp2f(zz.y)};
+  const mlic_float2 m = {__builtin_fmaxf(x.x, 0.0f), __builtin_fmaxf(x.y, 0.0f)};
+  return m - ax * (q * e);
+}
 // the conv / depthwise epilogues' GELU: torch's own formula 0.5 x (1 + erf(x / sqrt 2)) on the
 // library erff.  Its branches keep those epilogues' fully unrolled element loops small (the
 // branch-free gelu_erf, evaluated for every element there, pushes them past the unroller's budget or

@@ -28,6 +28,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace mlic {
 
 namespace {
@@ -313,6 +315,9 @@ __global__ __launch_bounds__(DR_THREADS) void dwpw_kernel(ConvParams P, const _F
 // Workgroup tile = 4 rows x 60 columns (wave w: row y0 + w), dealt XCD-aware as dwpw_kernel's.
 // Needs W even (a lane's pixel pair is either inside the row or entirely outside it) and an even
 // number of 16-channel k-steps (the ring's slot of a k-step is static across tiles).
+#ifndef MLIC_DPABL  // diagnostics build: 1 = one MFMA per k-step, 2 = no depthwise math, 4 = no output stores
+#define MLIC_DPABL 0
+#endif
 constexpr int DP_WAVES = 4;
 constexpr int DP_THREADS = DP_WAVES * 64;
 constexpr int DP_SEG = 60;
@@ -320,6 +325,7 @@ constexpr int DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138;
 
 namespace {
 typedef float float2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 // lane - 1 (SHR) / lane + 1 (SHL) of the whole wave; lane 0 / 63 receive 0 (never used)
 template <int CTRL>
 __device__ __forceinline__ float wave_nb(float v) {
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _
   constexpr int ROWS = CT * 32;
   constexpr int TAPB = CIN * DR_DWP * 4 + ROWS * 4;
   constexpr int LDS = TAPB + KS * ROWS * 64;
-  static_assert(CIN % 32 == 0 && LDS <= 160 * 1024, "dwpw2: LDS / even k-steps");
+  static_assert(CIN % 16 == 0 && LDS <= 160 * 1024, "dwpw2: LDS");
   __shared__ __attribute__((aligned(16))) char sm[LDS];
   float* sdw = reinterpret_cast<float*>(sm);
   float* sbias = sdw + CIN * DR_DWP;
@@ -418,71 +424,110 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _
     }
   };
 
-  float2v ring[2][8][3];  // k-step j in slot j & 1
+  // LDS offsets (kept as integers so the LDS address space survives the opaque redefinitions below)
+  uint32_t tapo = 8 * h * DR_DWP;  // floats: the lane half's channels 8h.. of each k-step
+  uint32_t abo = n * 64;           // bytes: A image row n of k-step 0
+  // depthwise 3x3 of channel 16j + 8h + i (k-step j) at the lane's two pixels (dw3x3's order); the
+  // channel's ring registers are refilled, as soon as they are read, with the same channel of the
+  // k-step two ahead (segment s, channel offset so)
+  auto dw_channel = [&](float2v (&rk)[3], int j, int i, const Seg2& s, uint32_t so) {
+    const float4* tq = reinterpret_cast<const float4*>(sdw + tapo + (16 * j + i) * DR_DWP);
+    const float4 w0 = tq[0], w1 = tq[1];
+    const float2 w2 = *reinterpret_cast<const float2*>(tq + 2);
+    const float tw[10] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y};
+    float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float p0 = rk[dy].x, p1 = rk[dy].y;
+      a0 = fmaf(tw[3 * dy + 0], wave_nb<DPP_WAVE_SHR1>(p1), a0);
+      a0 = fmaf(tw[3 * dy + 1], p0, a0);
+      a0 = fmaf(tw[3 * dy + 2], p1, a0);
+      a1 = fmaf(tw[3 * dy + 0], p0, a1);
+      a1 = fmaf(tw[3 * dy + 1], p1, a1);
+      a1 = fmaf(tw[3 * dy + 2], wave_nb<DPP_WAVE_SHL1>(p0), a1);
+    }
+    float2v v = {a0 + tw[9], a1 + tw[9]};
+    if (MLIC_DPABL & 2) v = rk[1];  // diagnostics: no depthwise math
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+      rk[dy] = __builtin_bit_cast(float2v, __builtin_amdgcn_raw_buffer_load_b64(s.rs, s.vo[dy], so, 0));
+    return v;
+  };
+  // channels i, i + 1 of k-step j split into the hi / lo B fragments of pixel e = 0, 1: one packed
+  // conversion per fragment register (v_cvt_pk_f16_f32), the residual of both in one packed add
+  auto dw_pair = [&](float2v (&r0)[3], float2v (&r1)[3], int j, int i, half8 (&bh)[2], half8 (&bl)[2], const Seg2& s,
+                     uint32_t so) {
+    uint32_t so1 = so + hw4;
+    dr_opaque(so1);
+    const float2v c0 = dw_channel(r0, j, i, s, so);
+    const float2v c1 = dw_channel(r1, j, i + 1, s, so1);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float2v v = {c0[e], c1[e]};
+      const half2v hv = __builtin_convertvector(v, half2v);
+      const half2v lv = __builtin_convertvector(v - __builtin_convertvector(hv, float2v), half2v);
+      bh[e][i] = hv[0];
+      bh[e][i + 1] = hv[1];
+      bl[e][i] = lv[0];
+      bl[e][i + 1] = lv[1];
+    }
+  };
+
+  // pipeline: k-step j + 1's depthwise + split runs interleaved with k-step j's MFMAs (a channel pair
+  // per CT * 6 / 4 MFMAs, in program order) and refills the one-slot register ring with k-step j + 2
+  // (of this tile, or of the next one: the ring and the B fragments carry across tiles)
+  float2v ring[8][3];
   Seg2 cur = seg_of(tile);
   int nt = tile + nslot < t_end ? tile + nslot : tile;
   Seg2 nxt = seg_of(nt);
-  load_ks(ring[0], cur, 0);
+  load_ks(ring, cur, 0);
+  half8 bh[2], bl[2];
+#pragma unroll
+  for (int i = 0; i < 8; i += 2)
+    dw_pair(ring[i], ring[i + 1], 0, i, bh, bl, KS > 1 ? cur : nxt, (uint32_t)(KS > 1 ? 16 + i : i) * hw4);
 
   const int swz = dr_swz(n);
   const int gh = (h ^ swz) << 4, gl = ((2 + h) ^ swz) << 4;
   bool bad = false;
-  for (;;) {
-    floatx16 acc[CT][2];
+  floatx16 acc[CT][2];
+  // k-step j: its MFMAs (the first k-step of a tile starts from a zero accumulator: an inline-constant
+  // C operand, no zeroing moves) interleaved with k-step j + 1's depthwise
+  auto kstep = [&](int j, auto first) {
+    // the ring holds k-step j + 1 (of this tile, or the next tile's k-step 0 when j = KS - 1); its
+    // refill is k-step j + 2 (wrapping into the next tile the same way)
+    const int j1 = (j + 1) % KS, j2 = j + 2;
+    const Seg2& s2 = j2 < KS ? cur : nxt;
+    const uint32_t so2 = (uint32_t)(16 * (j2 < KS ? j2 : j2 - KS)) * hw4;
+    half8 nbh[2], nbl[2];
+    // the LDS offsets are redefined per k-step: otherwise the compiler hoists the tap and A-fragment
+    // reads of later k-steps (LDS is never written here) and spills them
+    asm volatile("" : "+v"(tapo), "+v"(abo));
+    const char* ab = sa + abo + j * ROWS * 64;
+    constexpr int NM = MLIC_DPABL & 1 ? 1 : CT * 6;  // MFMAs per k-step
 #pragma unroll
-    for (int c = 0; c < CT; ++c)
+    for (int i = 0; i < 8; i += 2) {
+      dw_pair(ring[i], ring[i + 1], j1, i, nbh, nbl, s2, so2 + (uint32_t)i * hw4);
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[c][e][r] = 0.0f;
-
-#pragma unroll
-    for (int j = 0; j < KS; ++j) {
-      // the next k-step's loads (this segment's j + 1, or the next segment's k-step 0) go out first:
-      // their slot was consumed by k-step j - 1
-      if (j + 1 < KS) load_ks(ring[(j + 1) & 1], cur, (uint32_t)(16 * (j + 1)) * hw4);
-      else load_ks(ring[0], nxt, 0u);
-      float2v (&rk)[8][3] = ring[j & 1];
-      half8 bh[2], bl[2];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        // depthwise 3x3 of channel 16j + 8h + i at the lane's two pixels, dw3x3's order
-        const float4* tq = reinterpret_cast<const float4*>(sdw + (16 * j + 8 * h + i) * DR_DWP);
-        const float4 w0 = tq[0], w1 = tq[1];
-        const float2 w2 = *reinterpret_cast<const float2*>(tq + 2);
-        const float tw[10] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y};
-        float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const float p0 = rk[i][dy].x, p1 = rk[i][dy].y;
-          a0 = fmaf(tw[3 * dy + 0], wave_nb<DPP_WAVE_SHR1>(p1), a0);
-          a0 = fmaf(tw[3 * dy + 1], p0, a0);
-          a0 = fmaf(tw[3 * dy + 2], p1, a0);
-          a1 = fmaf(tw[3 * dy + 0], p0, a1);
-          a1 = fmaf(tw[3 * dy + 1], p1, a1);
-          a1 = fmaf(tw[3 * dy + 2], wave_nb<DPP_WAVE_SHL1>(p0), a1);
-        }
-        const float v0 = a0 + tw[9], v1 = a1 + tw[9];
-        const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
-        bh[0][i] = h0;
-        bh[1][i] = h1;
-        bl[0][i] = (_Float16)(v0 - (float)h0);
-        bl[1][i] = (_Float16)(v1 - (float)h1);
-      }
-      const char* ab = sa + (j * ROWS + n) * 64;
-#pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        const half8 ah = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gh);
-        const half8 al = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gl);
+      for (int t = (i / 2) * NM / 4; t < (i / 2 + 1) * NM / 4; ++t) {
+        const int c = (MLIC_DPABL & 1) ? 0 : t / 6, r = t % 6, e = r & 1;
         // pw_resident's term order per accumulator: lo.hi, hi.lo, hi.hi
-        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[0], acc[c][0], 0, 0, 0);
-        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[1], acc[c][1], 0, 0, 0);
-        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[0], acc[c][0], 0, 0, 0);
-        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[1], acc[c][1], 0, 0, 0);
-        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[0], acc[c][0], 0, 0, 0);
-        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[1], acc[c][1], 0, 0, 0);
+        const half8 av = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + (r < 2 ? gl : gh));
+        half8 bv = r >= 2 && r < 4 ? bl[e] : bh[e];
+        if (MLIC_DPABL & 1) bv = bh[0] + bl[0] + bh[1] + bl[1];  // diagnostics: one MFMA per k-step
+        const bool zero = decltype(first)::value && r < 2;
+        acc[c][e] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, zero ? floatx16{} : acc[c][e], 0, 0, 0);
       }
     }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      bh[e] = nbh[e];
+      bl[e] = nbl[e];
+    }
+  };
+  for (;;) {
+    kstep(0, std::true_type{});
+#pragma nounroll
+    for (int j = 1; j < KS; ++j) kstep(j, std::false_type{});
 
     // epilogue (pw_resident's op sequence): bias, range guard, GELU, residual; pixel pairs as dwordx2
     {
@@ -516,25 +561,44 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _
 #pragma unroll
           for (int g = 0; g < 4; ++g) bq[g] = *reinterpret_cast<const float4*>(sb + c * 32 + 8 * g);
           oo = so_o;
+          float2v vv[16];
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
-            const int co = c * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-            if (q > 0) {
-              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;
-              dr_opaque(oo);
-            }
             const float4 b4 = bq[q >> 2];
             const float bv = (q & 3) == 0 ? b4.x : (q & 3) == 1 ? b4.y : (q & 3) == 2 ? b4.z : b4.w;
-            float2v v;
+            float2v t = float2v{ldexpf(acc[c][0][q], -wexp), ldexpf(acc[c][1][q], -wexp)} + bv;
+            if (GELU) t = gelu_erf2(t);
+            vv[q] = t + xr[q];
+          }
+          // range guard: a split operand beyond fp16 makes its accumulator inf / NaN, which survives
+          // the epilogue and this fixed-order sum of the co-tile's outputs (a finite overflow of the
+          // sum only errs to the safe side: the exact-fp32 fallback)
+          float2v sum = vv[0];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              float t = ldexpf(acc[c][e][q], -wexp) + bv;
-              bad |= !(fabsf(t) <= 3.4e38f);
-              if (GELU) t = gelu_erf(t);
-              v[e] = t + xr[q][e];
+          for (int q = 1; q < 16; ++q) sum += vv[q];
+          bad |= !(fabsf(sum.x) <= 3.4e38f) || !(fabsf(sum.y) <= 3.4e38f);
+          if (MLIC_DPABL & 4) {  // diagnostics: epilogue math without the stores
+#pragma unroll
+            for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(vv[q][0]), "v"(vv[q][1]));
+          } else if (c * 32 + 32 <= P.Cout) {  // uniform: a whole co-tile, straight-line stores
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              if (q > 0) {
+                oo += (((q & 3) == 0) ? 5u : 1u) * cs4;
+                dr_opaque(oo);
+              }
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, vv[q]), rs_out, vo_out, oo, 0);
             }
-            if (c * 32 + 32 <= P.Cout || co < P.Cout)
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs_out, vo_out, oo, 0);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              if (q > 0) {
+                oo += (((q & 3) == 0) ? 5u : 1u) * cs4;
+                dr_opaque(oo);
+              }
+              if (c * 32 + (q & 3) + 8 * (q >> 2) + 4 * h < P.Cout)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, vv[q]), rs_out, vo_out, oo, 0);
+            }
           }
           so_o += 32 * cs4;
           dr_opaque(so_o);
