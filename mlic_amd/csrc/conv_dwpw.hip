@@ -4,27 +4,38 @@
 // stride-1 dwsep conv of their residual blocks (res_blk.py:62-154: ResidualBlock conv1 / conv2,
 // ResidualBlockWithStride conv2, ResidualBlockUpsample conv): Cin = Cout = N.
 //
-// Barrier-free form of the resident pointwise kernel (conv_pw.hip pw_resident_kernel).  One workgroup
-// per CU keeps, for its whole life, in LDS:
+// Barrier-free, like the resident pointwise kernel (conv_pw.hip pw_resident_kernel).  One workgroup
+// of 4 waves (one per SIMD) per CU keeps, for its whole life, in LDS:
 //   * the split hi/lo pointwise weights as an MFMA A-fragment image, [k-step][row][64 B] with the four
 //     16-byte granules (hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15) XOR-swizzled by (row >> 2) & 3:
 //     conflict-free ds_read_b128 for both lane groups (no padding, so N = 192 fits beside the taps);
 //   * the depthwise taps + bias, [C][12] floats, read by broadcast ds_read_b128.
-// Each of its 8 waves then walks its own 32-pixel row segments with no workgroup barrier (the waves of a
-// workgroup take the 8 rows of one 8 x 32 tile, so a row's three readers share the CU's L1): lane l32 is
-// column x0 + l32, lane half h holds channels 8h..8h+7 of a 16-deep k-step (the B fragment of
-// v_mfma_f32_32x32x16_f16).  Per channel the lane loads its column of the 3 input rows, and its
-// horizontal neighbours come from the adjacent lanes by DPP row shifts; the lanes at the ends of each
-// 16-lane DPP row take the neighbour from a second (edge) load whose address only they need
-// (x - 1 at columns 0 / 16, x + 1 at columns 15 / 31).  Out-of-image taps read 0 through an
-// out-of-range buffer offset.  The depthwise sum is dw3x3_s1_vec_kernel's order (acc = 0, taps
-// row-major by fma, + bias), so the B operand equals the unfused depthwise output bit for bit, and
-// the MFMA k order is pw_resident's: the fused output equals depthwise + resident pointwise bit for
-// bit (tests/test_gpu_conv.py::test_dwpw_fused).  Loads run one k-step ahead in a register ring that
-// carries across row segments.  Tiles are dealt XCD-aware: the workgroups of one XCD (blockIdx % 8
-// under round-robin placement; speed only) take one contiguous eighth of them.
+// Every lane owns TWO adjacent pixels of one row: its activation loads are dwordx2 (8 B per lane per
+// channel and row), and the two pixels are the columns of two v_mfma_f32_32x32x16_f16 B fragments
+// (e = 0, 1: column n <-> pixel xl + e; lane half h holds channels 8h..8h+7 of a 16-deep k-step), whose
+// accumulators hold, lane for lane, the same output channel of both pixels -- the epilogue stores them
+// as dwordx2 too.  A wave row segment is 64 loaded columns (lane n: xl = x0 - 2 + 2n) for 60 output
+// columns: lanes 0 and 31 of each lane half only supply the halo (x0 - 1 via lane 0's second pixel,
+// x0 + 60 via lane 31's first) and store nothing, so the horizontal neighbours are plain DPP wave
+// shifts with no edge loads (what a halo lane receives across the lane-half seam is never used); MFMA
+// columns wasted: 2 of 32.  Out-of-image taps read 0 through an out-of-range buffer offset.
+// The depthwise sum is dw3x3_s1_vec_kernel's order (acc = 0, taps row-major by fma, + bias), the hi /
+// lo split and the MFMA k order are pw_resident's, and the epilogue is pw_resident's op sequence
+// (gelu_erf2 is gelu_erf element for element): the fused output equals depthwise + resident pointwise
+// bit for bit (tests/test_gpu_conv.py::test_dwpw_fused).
+// Pipeline: k-step j + 1's depthwise + split runs interleaved with k-step j's MFMAs in program order,
+// and refills a one-slot register ring with k-step j + 2 channel by channel; the ring and the B
+// fragments carry across tiles.  The accumulators of all Cout rows (CT x 2 x 16 registers, AGPRs)
+// take one wave per SIMD.  Workgroup tile = 4 rows x 60 columns (wave w: row y0 + w); tiles ordered
+// (image, row block, segment) and dealt XCD-aware (the workgroups of one XCD, blockIdx % 8 under
+// round-robin placement, take one contiguous eighth of them: speed only).  Needs W even (a lane's
+// pixel pair is either inside the row or entirely outside it).
 // HBM bytes per pixel: 4 * (Cin + Cout [+ Cout residual]) -- the pointwise conv's alone; the unfused
-// pair moves 4 * (3 Cin + Cout [+ Cout]).
+// pair moves 4 * (3 Cin + Cout [+ Cout]).  Measured (8 x 192 x 544 x 960, GELU): 2.42-2.49 ms against
+// 2.98 ms for depthwise + resident pointwise.  Rejected: the lane-per-pixel form (b32 main + edge loads,
+// 8 waves: 3.2 ms); the same kernel without its depthwise stage as a pointwise conv (1.81 vs 1.68 ms
+// for pw_resident, one wave per SIMD cannot hide the epilogue); a barrier per k-step to keep the four
+// row waves in step for L1 reuse (-16 % L2 requests, +5 % time).
 #include "common.h"
 #include "kernels.h"
 
@@ -38,11 +49,8 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int DR_WAVES = 8;
-constexpr int DR_THREADS = DR_WAVES * 64;
 constexpr int DR_DWP = 12;                 // floats per depthwise channel in LDS: 9 taps, bias, 2 pad
 constexpr uint32_t DR_OOB = 0x80000000u;   // buffer offset past any image: the load returns 0
-constexpr int DPP_ROW_SHL1 = 0x101, DPP_ROW_SHR1 = 0x111;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dr_rsrc(const float* base, uint32_t bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
@@ -55,266 +63,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dr_rsrc(const float* base, uin
 __device__ __forceinline__ void dr_opaque(uint32_t& v) { asm volatile("" : "+s"(v)); }
 __device__ __forceinline__ int dr_swz(int row) { return (row >> 2) & 3; }
 
-// neighbour of this lane's value from lane - 1 (SHR) / lane + 1 (SHL) of its 16-lane DPP row; the
-// first / last lane of the row keeps `edge`
-template <int CTRL>
-__device__ __forceinline__ float dpp_nb(float edge, float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, edge), __builtin_bit_cast(int, v),
-                                                                CTRL, 0xF, 0xF, false));
-}
 }  // namespace
 
-template <int CIN, int CT, bool GELU, bool RES>
-__global__ __launch_bounds__(DR_THREADS) void dwpw_kernel(ConvParams P, const _Float16* __restrict__ wh,
-                                                        const _Float16* __restrict__ wl, int cin_pad,
-                                                        const float* __restrict__ dww, const float* __restrict__ dwb) {
-  constexpr int KS = CIN / 16;
-  constexpr int ROWS = CT * 32;
-  constexpr int TAPB = CIN * DR_DWP * 4 + ROWS * 4;  // taps + bias first: small ds_read offsets
-  constexpr int LDS = TAPB + KS * ROWS * 64;
-  static_assert(CIN % 16 == 0 && LDS <= 160 * 1024, "dwpw: LDS");
-  __shared__ __attribute__((aligned(16))) char sm[LDS];
-  float* sdw = reinterpret_cast<float*>(sm);
-  float* sbias = sdw + CIN * DR_DWP;
-  char* sa = sm + TAPB;
-
-  const int tid = threadIdx.x;
-  {  // prologue: every weight load in flight before the first LDS store (one memory latency)
-    constexpr int NG = KS * ROWS * 4;  // 16-byte granules of the A image
-    constexpr int NIT = (NG + DR_THREADS - 1) / DR_THREADS;
-    u32x4 st[NIT];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int id = tid + it * DR_THREADS;
-      const int q = id & 3, row = (id >> 2) % ROWS, j = (id >> 2) / ROWS;
-      st[it] = u32x4{0u, 0u, 0u, 0u};
-      if (id < NG && row < P.Cout)
-        st[it] = *reinterpret_cast<const u32x4*>((q < 2 ? wh : wl) + (int64_t)row * cin_pad + 16 * j + 8 * (q & 1));
-    }
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int id = tid + it * DR_THREADS;
-      const int q = id & 3, row = (id >> 2) % ROWS, j = (id >> 2) / ROWS;
-      if (id < NG) *reinterpret_cast<u32x4*>(sa + (j * ROWS + row) * 64 + ((q ^ dr_swz(row)) << 4)) = st[it];
-    }
-  }
-  for (int i = tid; i < CIN * DR_DWP; i += DR_THREADS) {
-    const int c = i / DR_DWP, k = i - c * DR_DWP;
-    sdw[i] = k < 9 ? dww[c * 9 + k] : (k == 9 && dwb ? dwb[c] : 0.0f);
-  }
-  for (int r = tid; r < ROWS; r += DR_THREADS) sbias[r] = (P.bias && r < P.Cout) ? P.bias[r] : 0.0f;
-  __syncthreads();  // the only barrier
-
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, h = lane >> 5;
-  const int H = P.H, W = P.W, HW = H * W;
-  // workgroup tile = DR_WAVES rows x 32 columns (wave w: row y0 + w), so a row's three readers are
-  // waves of one CU, reading it while its lines are in that CU's L1; tiles ordered (image, row
-  // block, segment) and dealt XCD-aware (a multiple of 8 workgroups: blocks b and b + 8 share an XCD
-  // under round-robin placement, speed only): one XCD takes a contiguous run of tiles, so the
-  // horizontal neighbours' edge lines and the next row block's halo rows are L2 neighbours
-  const int nseg = (W + 31) >> 5;
-  const int nyb = (H + DR_WAVES - 1) / DR_WAVES;
-  const int tpi = nseg * nyb;  // workgroup tiles per image
-  const int ntiles = tpi * P.B;
-  const int xcd = (int)blockIdx.x & 7, nslot = (int)gridDim.x >> 3;
-  const int t_end = (int)((int64_t)(xcd + 1) * ntiles / 8);
-  const int tstride = nslot;
-  int tile = (int)((int64_t)xcd * ntiles / 8) + ((int)blockIdx.x >> 3);
-  if (tile >= t_end) return;  // the whole workgroup: no barrier follows
-
-  const uint32_t hw4 = (uint32_t)HW * 4u;
-  const uint32_t img_bytes = (uint32_t)CIN * hw4;
-  const float* xbase = P.seg[0].p;
-  const int64_t xbs = P.seg[0].bs;
-  const int xe_d = (l32 & 15) == 0 ? -1 : ((l32 & 15) == 15 ? 1 : 0);  // the edge lanes' neighbour
-
-  // per segment: 3 main + 3 edge byte offsets (the lane half's channel 8h folded in)
-  struct Seg {
-    __amdgpu_buffer_rsrc_t rs;
-    uint32_t vm[3], ve[3];
-  };
-  auto seg_of = [&](int t) {
-    Seg s;
-    const int b = t / tpi;
-    const int r = t - b * tpi;
-    const int yb = r / nseg;
-    const int y = yb * DR_WAVES + wave;  // rows past the image read 0 and store nothing
-    const int x = ((r - yb * nseg) << 5) + l32, xe = x + xe_d;
-    s.rs = dr_rsrc(xbase + (int64_t)b * xbs, img_bytes);
-    const uint32_t ch = (uint32_t)(8 * h) * hw4;
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      const int yy = y + dy - 1;
-      const bool ok = yy >= 0 && yy < H;
-      s.vm[dy] = ok && x < W ? (uint32_t)(yy * W + x) * 4u + ch : DR_OOB;
-      s.ve[dy] = ok && xe >= 0 && xe < W ? (uint32_t)(yy * W + xe) * 4u + ch : DR_OOB;
-    }
-    return s;
-  };
-  // a unit = 4 channel slots of a k-step (half of the lane's 8): main + edge loads of 3 rows each
-  // (24 loads); units are loaded 2 ahead (one k-step), so at most 48 loads are outstanding per wave
-  // (the vmcnt counter holds 63) and each unit waits for exactly its own loads
-  auto load_unit = [&](float (&r)[4][3], float (&e)[4][3], const Seg& s, uint32_t so) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        r[i][dy] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.rs, s.vm[dy], so, 0));
-        e[i][dy] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s.rs, s.ve[dy], so, 0));
-      }
-      so += hw4;
-      dr_opaque(so);
-    }
-  };
-
-  float rm[2][4][3], re[2][4][3];  // ring: unit u in slot u & 1
-  Seg cur = seg_of(tile);
-  int nt = tile + tstride < t_end ? tile + tstride : tile;
-  Seg nxt = seg_of(nt);
-  load_unit(rm[0], re[0], cur, 0);
-  load_unit(rm[1], re[1], cur, 4 * hw4);
-
-  const int swz = dr_swz(l32);  // rows 32c + l32 share the swizzle of l32
-  const int gh = (h ^ swz) << 4, gl = ((2 + h) ^ swz) << 4;
-  bool bad = false;
-  for (;;) {
-    floatx16 acc[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
-
-#pragma unroll 2
-    for (int j = 0; j < KS; ++j) {
-      // the next k-step's loads: this segment's j + 1, or the next segment's k-step 0
-      const bool last = j + 1 == KS;
-      const Seg& ns = last ? nxt : cur;
-      const uint32_t so_next = last ? 0u : (uint32_t)(16 * (j + 1)) * hw4;
-      half8 bh, bl;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        // depthwise 3x3 of the lane's channels 16j + 8h + 4u + i at its pixel, split hi / lo
-        const float* tq0 = sdw + (16 * j + 8 * h + 4 * u) * DR_DWP;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float4* tq = reinterpret_cast<const float4*>(tq0 + i * DR_DWP);
-          const float4 w0 = tq[0], w1 = tq[1];
-          const float2 w2 = *reinterpret_cast<const float2*>(tq + 2);  // ds_read_b128 x 2 + b64
-          const float tw[10] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y};
-          float a = 0.0f;
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy) {
-            const float m = rm[u][i][dy], e = re[u][i][dy];
-            a = fmaf(tw[3 * dy + 0], dpp_nb<DPP_ROW_SHR1>(e, m), a);
-            a = fmaf(tw[3 * dy + 1], m, a);
-            a = fmaf(tw[3 * dy + 2], dpp_nb<DPP_ROW_SHL1>(e, m), a);
-          }
-          const float v = a + tw[9];
-          const _Float16 hv = (_Float16)v;
-          bh[4 * u + i] = hv;
-          bl[4 * u + i] = (_Float16)(v - (float)hv);
-        }
-        uint32_t so = so_next + (uint32_t)(4 * u) * hw4;
-        dr_opaque(so);
-        load_unit(rm[u], re[u], ns, so);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the refills behind the depthwise math, ahead of the MFMAs
-      const char* ab = sa + (j * ROWS + l32) * 64;
-#pragma unroll
-      for (int c = 0; c < CT; c += 2) {
-        const int c1 = (c + 1 < CT) ? c + 1 : c;
-        const half8 ah0 = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gh);
-        const half8 al0 = *reinterpret_cast<const half8*>(ab + c * 32 * 64 + gl);
-        const half8 ah1 = *reinterpret_cast<const half8*>(ab + c1 * 32 * 64 + gh);
-        const half8 al1 = *reinterpret_cast<const half8*>(ab + c1 * 32 * 64 + gl);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al0, bh, acc[c], 0, 0, 0);
-        if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al1, bh, acc[c1], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bl, acc[c], 0, 0, 0);
-        if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bl, acc[c1], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bh, acc[c], 0, 0, 0);
-        if (c1 != c) acc[c1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bh, acc[c1], 0, 0, 0);
-      }
-    }
-
-    // epilogue (pw_resident's): bias, range guard, GELU, residual; one segment of 32 columns
-    {
-      const int b = tile / tpi;
-      const int r = tile - b * tpi;
-      const int yb = r / nseg;
-      const int y = yb * DR_WAVES + wave;
-      const int x = ((r - yb * nseg) << 5) + l32;
-      if (x < W && y < H) {
-        const uint32_t cs4 = (uint32_t)P.out_cs * 4u;
-        const uint32_t vo_out = (uint32_t)(y * W + x) * 4u + (uint32_t)(4 * h) * cs4;
-        const auto rs_out = dr_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
-        const auto rs_res = dr_rsrc(RES ? P.res + (int64_t)b * P.res_bs : P.out, RES ? (uint32_t)P.Cout * cs4 : 0u);
-        const float* sb = sbias + 4 * h;
-        const int wexp = P.wexp;
-        uint32_t so_o = 0;
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          float xr[16];
-          uint32_t oo = so_o;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            if (q > 0) {
-              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;  // co_u = 32c + (q&3) + 8(q>>2)
-              dr_opaque(oo);
-            }
-            xr[q] = RES ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, vo_out, oo, 0)) : 0.0f;
-          }
-          float4 bq[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) bq[g] = *reinterpret_cast<const float4*>(sb + c * 32 + 8 * g);
-          oo = so_o;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int co = c * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-            if (q > 0) {
-              oo += (((q & 3) == 0) ? 5u : 1u) * cs4;
-              dr_opaque(oo);
-            }
-            const float4 b4 = bq[q >> 2];
-            const float bv = (q & 3) == 0 ? b4.x : (q & 3) == 1 ? b4.y : (q & 3) == 2 ? b4.z : b4.w;
-            float v = ldexpf(acc[c][q], -wexp) + bv;
-            bad |= !(fabsf(v) <= 3.4e38f);
-            if (GELU) v = gelu_erf(v);
-            v += xr[q];
-            if (c * 32 + 32 <= P.Cout || co < P.Cout)
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs_out, vo_out, oo, 0);
-          }
-          so_o += 32 * cs4;
-          dr_opaque(so_o);
-        }
-      }
-    }
-    if (nt == tile) break;
-    tile = nt;
-    cur = nxt;
-    nt = tile + tstride < t_end ? tile + tstride : tile;
-    nxt = seg_of(nt);
-  }
-  range_report(P.rflag, bad);
-}
-
-// -------------------------------------------------------------------------------------------------
-// Pixel-pair form (default).  Same LDS-resident weights and depthwise order as dwpw_kernel above,
-// but every lane owns TWO adjacent pixels of one row: its activation loads are dwordx2 (8 B per lane
-// per channel and row: a quarter of dwpw_kernel's vector-memory instructions per pixel, whose main +
-// edge b32 loads were its issue limit), and the two pixels are the columns of two MFMA B fragments
-// (e = 0, 1: column n <-> pixel xl + e), whose accumulators hold, lane for lane, the same output
-// channel of both pixels -- the epilogue stores them as dwordx2 too.
-// A wave row segment is 64 loaded columns (lane n: xl = x0 - 2 + 2n) for 60 output columns: lanes
-// 0 and 31 of each lane half only supply the halo (x0 - 1 via lane 0's second pixel, x0 + 60 via lane
-// 31's first) and store nothing, so the horizontal neighbours are plain DPP wave shifts with no edge
-// loads (the neighbour a halo lane receives across the lane-half seam is never used).  MFMA columns
-// wasted: 2 of 32.  One wave per SIMD (4 waves, 256 threads, one workgroup per CU): the two-pixel
-// accumulators of all Cout rows (CT x 2 x 16 registers) live beside a two-k-step load ring.
-// Workgroup tile = 4 rows x 60 columns (wave w: row y0 + w), dealt XCD-aware as dwpw_kernel's.
-// Needs W even (a lane's pixel pair is either inside the row or entirely outside it) and an even
-// number of 16-channel k-steps (the ring's slot of a k-step is static across tiles).
 #ifndef MLIC_DPABL  // diagnostics build: 1 = one MFMA per k-step, 2 = no depthwise math, 4 = no output stores
 #define MLIC_DPABL 0
 #endif
@@ -334,14 +84,14 @@ __device__ __forceinline__ float wave_nb(float v) {
 }  // namespace
 
 template <int CIN, int CT, bool GELU, bool RES>
-__global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _Float16* __restrict__ wh,
+__global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _Float16* __restrict__ wh,
                                                          const _Float16* __restrict__ wl, int cin_pad,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb) {
   constexpr int KS = CIN / 16;
   constexpr int ROWS = CT * 32;
   constexpr int TAPB = CIN * DR_DWP * 4 + ROWS * 4;
   constexpr int LDS = TAPB + KS * ROWS * 64;
-  static_assert(CIN % 16 == 0 && LDS <= 160 * 1024, "dwpw2: LDS");
+  static_assert(CIN % 16 == 0 && LDS <= 160 * 1024, "dwpw: LDS");
   __shared__ __attribute__((aligned(16))) char sm[LDS];
   float* sdw = reinterpret_cast<float*>(sm);
   float* sbias = sdw + CIN * DR_DWP;
@@ -446,7 +196,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _
       a1 = fmaf(tw[3 * dy + 1], p1, a1);
       a1 = fmaf(tw[3 * dy + 2], wave_nb<DPP_WAVE_SHL1>(p0), a1);
     }
-    float2v v = {a0 + tw[9], a1 + tw[9]};
+    float2v v = float2v{a0 + tw[9], a1 + tw[9]};
     if (MLIC_DPABL & 2) v = rk[1];  // diagnostics: no depthwise math
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
@@ -499,6 +249,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw2_kernel(ConvParams P, const _
     const Seg2& s2 = j2 < KS ? cur : nxt;
     const uint32_t so2 = (uint32_t)(16 * (j2 < KS ? j2 : j2 - KS)) * hw4;
     half8 nbh[2], nbl[2];
+    if (MLIC_DPABL & 8) __builtin_amdgcn_s_barrier();  // experiment: keep the 4 row waves in step (L1 reuse)
     // the LDS offsets are redefined per k-step: otherwise the compiler hoists the tap and A-fragment
     // reads of later k-steps (LDS is never written here) and spills them
     asm volatile("" : "+v"(tapo), "+v"(abo));
@@ -631,7 +382,7 @@ static int dr_num_cus() {
 bool dwpw_ok(const ConvParams& P, int cin_pad) {
   if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.epi & ~(EPI_GELU | EPI_RES)) return false;
-  if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W) return false;
+  if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W || (P.W % 2) != 0) return false;
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
   const int ct = (P.Cout + 31) / 32;
@@ -645,12 +396,12 @@ bool dwpw_ok(const ConvParams& P, int cin_pad) {
 template <int CIN, int CT>
 static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                         const float* dwb, hipStream_t st) {
-  const int64_t want = (int64_t)((P.W + 31) / 32) * ((P.H + DR_WAVES - 1) / DR_WAVES) * P.B;  // workgroup tiles
+  const int64_t want = (int64_t)((P.W + DP_SEG - 1) / DP_SEG) * ((P.H + DP_WAVES - 1) / DP_WAVES) * P.B;
   const int64_t g = std::min<int64_t>(want, (int64_t)dr_num_cus());
   const dim3 grid((unsigned)((g + 7) / 8 * 8));  // a multiple of 8: the XCD-aware deal
   const bool gelu = (P.epi & EPI_GELU) != 0, res = (P.epi & EPI_RES) != 0;
 #define MLIC_DP(G, R) \
-  hipLaunchKernelGGL((dwpw_kernel<CIN, CT, G, R>), grid, dim3(DR_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
+  hipLaunchKernelGGL((dwpw_kernel<CIN, CT, G, R>), grid, dim3(DP_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
   if (gelu && res) MLIC_DP(true, true);
   else if (gelu) MLIC_DP(true, false);
   else if (res) MLIC_DP(false, true);
@@ -658,50 +409,14 @@ static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16*
 #undef MLIC_DP
   HIP_OK(hipGetLastError());
 }
-
-template <int CIN, int CT>
-static void launch_dwpw2(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
-                         const float* dwb, hipStream_t st) {
-  const int64_t want = (int64_t)((P.W + DP_SEG - 1) / DP_SEG) * ((P.H + DP_WAVES - 1) / DP_WAVES) * P.B;
-  const int64_t g = std::min<int64_t>(want, (int64_t)dr_num_cus());
-  const dim3 grid((unsigned)((g + 7) / 8 * 8));
-  const bool gelu = (P.epi & EPI_GELU) != 0, res = (P.epi & EPI_RES) != 0;
-#define MLIC_DP(G, R) \
-  hipLaunchKernelGGL((dwpw2_kernel<CIN, CT, G, R>), grid, dim3(DP_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
-  if (gelu && res) MLIC_DP(true, true);
-  else if (gelu) MLIC_DP(true, false);
-  else if (res) MLIC_DP(false, true);
-  else MLIC_DP(false, false);
-#undef MLIC_DP
-  HIP_OK(hipGetLastError());
-}
-
-// $MLIC_DWPW_V=1: the lane-per-pixel form (A/B only); default the pixel-pair form where it applies
-static int dwpw_version() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("MLIC_DWPW_V");
-    v = (e && e[0] == '1') ? 1 : 2;
-  }
-  return v;
-}
-
-static bool dwpw2_ok(const ConvParams& P) { return (P.W % 2) == 0 && (P.Cin % 32) == 0; }
 
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st) {
   MLIC_CHECK(dwpw_ok(P, cin_pad) && dww, "dwpw: unsupported shape");
-  const bool v2 = dwpw_version() == 2 && dwpw2_ok(P);
-#define DR_RUN(CIN, CT)                                              \
-  if (P.Cin == CIN) {                                                \
-    if constexpr (CIN % 32 == 0) {                                   \
-      if (v2) {                                                      \
-        launch_dwpw2<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st);     \
-        return;                                                      \
-      }                                                              \
-    }                                                                \
-    launch_dwpw<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st);          \
-    return;                                                          \
+#define DR_RUN(CIN, CT)                                     \
+  if (P.Cin == CIN) {                                       \
+    launch_dwpw<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st); \
+    return;                                                 \
   }
   DR_SHAPES(DR_RUN)
 #undef DR_RUN

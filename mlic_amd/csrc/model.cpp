@@ -432,12 +432,13 @@ bool Model::hoist_on() const {
   return on && chain_on() && hoist_.Cout > 0;
 }
 
-// $MLIC_DWPW=1: the fused dwpw kernel (conv_dwpw.hip) instead of depthwise + resident pointwise for
-// the stride-1 dwsep convs (A/B switch; the results are bit-identical)
+// the fused dwpw kernel (conv_dwpw.hip) instead of depthwise + resident pointwise for the stride-1
+// dwsep convs with an even width (default; $MLIC_DWPW=0 is the A/B switch; the results are
+// bit-identical either way)
 bool Model::dwpw_on() const {
   static const bool on = [] {
     const char* e = std::getenv("MLIC_DWPW");
-    return e && std::atoi(e) == 1;
+    return !(e && std::atoi(e) == 0);
   }();
   return on && prec() == PREC_F16X3_V2;
 }

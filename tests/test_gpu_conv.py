@@ -267,16 +267,15 @@ def test_depthwise(shape):
 
 
 @pytest.mark.parametrize("B,Cn,H,W,epi", [
-    (2, 192, 40, 100, 1),    # GELU; 100 columns = 3 segments of 32 + a ragged 4
-    (1, 192, 17, 61, 0),     # odd sizes, ragged last segment
+    (2, 192, 40, 100, 1),    # GELU; 100 columns = one 60-column segment + a ragged 40
+    (1, 192, 17, 61, 0),     # odd width: refused (the model runs it unfused)
     (2, 192, 68, 120, 1 | 64),  # latent grid, GELU + residual
     (1, 128, 24, 30, 0),     # Cin 128, one ragged segment
-    (3, 192, 20, 96, 64),    # residual only, exact 32-column segments
+    (3, 192, 20, 96, 64),    # residual only
     (2, 160, 9, 64, 1),      # MLICPP_M width
     (2, 96, 33, 70, 1 | 64), # MLICPP_S width
-    (2, 48, 16, 160, 1 | 64),  # the small-decoder model's g_s width (3 k-steps)
-    (1, 192, 1, 33, 1),      # a single row: both vertical taps out of the image
-    # pixel-pair form (even W): 60-column segments, 4-row workgroup tiles
+    (2, 48, 16, 160, 1 | 64),  # the small-decoder model's g_s width (3 k-steps: odd count)
+    (1, 192, 1, 34, 1),      # a single row: both vertical taps out of the image
     (2, 192, 13, 120, 1 | 64),  # two exact segments, ragged row block
     (1, 192, 6, 62, 0),      # one segment + one pixel pair
     (1, 96, 3, 2, 1),        # a single pair: both halo pairs out of the image
@@ -299,6 +298,12 @@ def test_dwpw_fused(B, Cn, H, W, epi):
     res = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
     st = torch.cuda.current_stream().cuda_stream
     y = torch.full((B, Cn, H, W), float("nan"), device=dev)
+    if W % 2:  # a lane's pixel pair must be inside the row or outside it: the model runs these unfused
+        with pytest.raises(_lib.MlicError):
+            _lib.call("mlic_dwpw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
+                      C.c_void_p(db.data_ptr()), C.c_void_p(w.data_ptr()), C.c_void_p(b.data_ptr()),
+                      C.c_void_p(y.data_ptr()), B, Cn, Cn, H, W, epi, C.c_void_p(res.data_ptr()))
+        return
     _lib.call("mlic_dwpw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
               C.c_void_p(db.data_ptr()), C.c_void_p(w.data_ptr()), C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()),
               B, Cn, Cn, H, W, epi, C.c_void_p(res.data_ptr()))
