@@ -83,7 +83,9 @@ __device__ __forceinline__ float wave_nb(float v) {
 }
 }  // namespace
 
-template <int CIN, int CT, bool GELU, bool RES>
+// MODE: 0 = bias only, 1 = GELU, 4 = 0.5 tanh + the checkerboard mask of P.epi (the LRP head), as
+// pw_resident's MODE; residual add (RES) last
+template <int CIN, int CT, int MODE, bool RES>
 __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _Float16* __restrict__ wh,
                                                          const _Float16* __restrict__ wl, int cin_pad,
                                                          const float* __restrict__ dww, const float* __restrict__ dwb) {
@@ -294,6 +296,12 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
         const auto rs_res = dr_rsrc(RES ? P.res + (int64_t)b * P.res_bs : P.out, RES ? (uint32_t)P.Cout * cs4 : 0u);
         const float* sb = sbias + 4 * h;
         const int wexp = P.wexp;
+        // checkerboard mask (MODE 4): keep a pixel where its anchor-ness matches the flag
+        bool keep[2] = {true, true};
+        if (MODE == 4 && (P.epi & (EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR))) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) keep[e] = is_anchor(y, xl + e) == ((P.epi & EPI_MASK_ANCHOR) != 0);
+        }
         uint32_t so_o = 0;
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
@@ -318,7 +326,11 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
             const float4 b4 = bq[q >> 2];
             const float bv = (q & 3) == 0 ? b4.x : (q & 3) == 1 ? b4.y : (q & 3) == 2 ? b4.z : b4.w;
             float2v t = float2v{ldexpf(acc[c][0][q], -wexp), ldexpf(acc[c][1][q], -wexp)} + bv;
-            if (GELU) t = gelu_erf2(t);
+            if constexpr (MODE == 1) t = gelu_erf2(t);
+            if constexpr (MODE == 4) {
+#pragma unroll
+              for (int e = 0; e < 2; ++e) t[e] = keep[e] ? 0.5f * tanhf(t[e]) : 0.0f;
+            }
             vv[q] = t + xr[q];
           }
           // range guard: a split operand beyond fp16 makes its accumulator inf / NaN, which survives
@@ -375,50 +387,66 @@ static int dr_num_cus() {
   return n;
 }
 
-// (CIN, CT) instantiated: Cin = Cout = N of g_a / g_s (MLICPP_L 192, M 160, S2 128, S 96, and the
-// small-decoder model's N / 4 = 48)
-#define DR_SHAPES(X) X(192, 6) X(160, 5) X(128, 4) X(96, 3) X(48, 2)
+// epilogue mode of P (the kernel's MODE), -1 when the kernel has none for it
+static int dw_mode(const ConvParams& P) {
+  const int e = P.epi & ~EPI_RES;
+  if (e == EPI_NONE) return 0;
+  if (e == EPI_GELU) return 1;
+  if (e == EPI_TANH_HALF || e == (EPI_TANH_HALF | EPI_MASK_ANCHOR) || e == (EPI_TANH_HALF | EPI_MASK_NONANCHOR))
+    return 4;
+  return -1;
+}
+
+// instantiated (CIN, CT, MODE, RES): Cin = Cout = N of g_a / g_s with every epilogue they use (MLICPP_L
+// 192, M 160, S2 128, S 96, the small-decoder model's N / 4 = 48); and the single-input dwsep convs of
+// the latent-resolution stacks (MLICPP_L, slice_ch 32): the LRP's 224 -> 128 GELU and 128 -> 32 head
+// (0.5 tanh, checkerboard mask, residual into y_hat; quantization.py:30-45), the channel context's
+// 192 -> 128 GELU (context.py:115-138) -- for the kernel-level tests and A/B only: at the latent grid
+// (8 K pixels per image) the per-workgroup weight prologue outweighs the saved bytes (LRP: 4.14 vs
+// 4.3 ms unfused per 8 images, channel context slower), so the model fuses only grids of >= 16 K
+// pixels per image (dwpw_grid_ok)
+#define DR_ALL(X, CIN, CT) X(CIN, CT, 0, 0) X(CIN, CT, 0, 1) X(CIN, CT, 1, 0) X(CIN, CT, 1, 1)
+#define DR_COMBOS(X)                                                                              \
+  DR_ALL(X, 192, 6) DR_ALL(X, 160, 5) DR_ALL(X, 128, 4) DR_ALL(X, 96, 3) DR_ALL(X, 48, 2)         \
+  X(224, 4, 1, 0) X(128, 1, 4, 1) X(192, 4, 1, 0)
+
+bool dwpw_grid_ok(const ConvParams& P) { return (int64_t)P.H * P.W >= 16384; }
 
 bool dwpw_ok(const ConvParams& P, int cin_pad) {
   if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
-  if (P.epi & ~(EPI_GELU | EPI_RES)) return false;
+  const int mode = dw_mode(P);
+  if (mode < 0) return false;
   if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W || (P.W % 2) != 0) return false;
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
-  const int ct = (P.Cout + 31) / 32;
-#define DR_OK(CIN, CT) \
-  if (P.Cin == CIN && ct == CT) return true;
-  DR_SHAPES(DR_OK)
+  const int ct = (P.Cout + 31) / 32, res = (P.epi & EPI_RES) ? 1 : 0;
+#define DR_OK(CIN, CT, M, R) \
+  if (P.Cin == CIN && ct == CT && mode == M && res == R) return true;
+  DR_COMBOS(DR_OK)
 #undef DR_OK
   return false;
 }
 
-template <int CIN, int CT>
+template <int CIN, int CT, int M, bool R>
 static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                         const float* dwb, hipStream_t st) {
   const int64_t want = (int64_t)((P.W + DP_SEG - 1) / DP_SEG) * ((P.H + DP_WAVES - 1) / DP_WAVES) * P.B;
   const int64_t g = std::min<int64_t>(want, (int64_t)dr_num_cus());
   const dim3 grid((unsigned)((g + 7) / 8 * 8));  // a multiple of 8: the XCD-aware deal
-  const bool gelu = (P.epi & EPI_GELU) != 0, res = (P.epi & EPI_RES) != 0;
-#define MLIC_DP(G, R) \
-  hipLaunchKernelGGL((dwpw_kernel<CIN, CT, G, R>), grid, dim3(DP_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb)
-  if (gelu && res) MLIC_DP(true, true);
-  else if (gelu) MLIC_DP(true, false);
-  else if (res) MLIC_DP(false, true);
-  else MLIC_DP(false, false);
-#undef MLIC_DP
+  hipLaunchKernelGGL((dwpw_kernel<CIN, CT, M, R>), grid, dim3(DP_THREADS), 0, st, P, wh, wl, cin_pad, dww, dwb);
   HIP_OK(hipGetLastError());
 }
 
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st) {
   MLIC_CHECK(dwpw_ok(P, cin_pad) && dww, "dwpw: unsupported shape");
-#define DR_RUN(CIN, CT)                                     \
-  if (P.Cin == CIN) {                                       \
-    launch_dwpw<CIN, CT>(P, wh, wl, cin_pad, dww, dwb, st); \
-    return;                                                 \
+  const int ct = (P.Cout + 31) / 32, mode = dw_mode(P), res = (P.epi & EPI_RES) ? 1 : 0;
+#define DR_RUN(CIN, CT, M, R)                                        \
+  if (P.Cin == CIN && ct == CT && mode == M && res == R) {           \
+    launch_dwpw<CIN, CT, M, R != 0>(P, wh, wl, cin_pad, dww, dwb, st); \
+    return;                                                          \
   }
-  DR_SHAPES(DR_RUN)
+  DR_COMBOS(DR_RUN)
 #undef DR_RUN
 }
 

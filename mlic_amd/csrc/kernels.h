@@ -39,6 +39,8 @@ void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 // fused depthwise 3x3 (stride 1, pad 1) + pointwise 1x1 (conv_dwpw.hip): P describes the pointwise
 // conv with the DEPTHWISE input as its input; dww [Cin][9], dwb [Cin]; needs W even (dwpw_ok)
 bool dwpw_ok(const ConvParams& P, int cin_pad);
+// the model's choice on top of dwpw_ok: grids where the fused kernel measured faster (per image only)
+bool dwpw_grid_ok(const ConvParams& P);
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st);
 

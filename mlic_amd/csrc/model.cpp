@@ -731,7 +731,7 @@ View Model::conv3x3(const std::vector<View>& ins, const std::string& p, int stri
   if (stride == 1 && dwpw_on() && w.wh && ins.size() == 1) {
     // fused: the pointwise conv reads the depthwise input; the depthwise output stays on chip
     ConvParams P = conv_params(ins, w, 1, 0, out, epi, nullptr, res);
-    if (dwpw_ok(P, w.cin_pad)) {
+    if (dwpw_ok(P, w.cin_pad) && dwpw_grid_ok(P)) {
       const double pix = (double)P.B * H * W;
       const double flops = 2.0 * pix * P.Cin * (9 + w.Cout);
       const double bytes = 4.0 * (pix * (P.Cin + w.Cout * (res ? 2 : 1)) + (double)w.Cout * P.Cin + 10.0 * P.Cin);

@@ -286,38 +286,58 @@ def test_dwpw_fused(B, Cn, H, W, epi):
     """Fused depthwise 3x3 + pointwise 1x1 (conv_dwpw.hip) == depthwise kernel then the resident-weight
     pointwise kernel, bit for bit (same depthwise order, same MFMA k order), and within the split-fp16
     tolerance of a float64 torch reference (DepthWiseConv, modules/layers/conv.py:22-32)."""
+    _dwpw_case(B, Cn, Cn, H, W, epi)
+
+
+# the latent-resolution dwsep convs with Cin != Cout: the LRP's 224 -> 128 GELU and its 128 -> 32 head
+# (0.5 tanh, checkerboard mask, residual; quantization.py:30-45), the channel context's 192 -> 128 GELU
+@pytest.mark.parametrize("B,Cin,Cout,H,W,epi", [
+    (2, 224, 128, 68, 120, 1), (1, 224, 128, 17, 30, 1),
+    (2, 128, 32, 68, 120, 8 | 16 | 64), (2, 128, 32, 17, 30, 8 | 32 | 64), (1, 128, 32, 9, 14, 8 | 16 | 64),
+    (2, 192, 128, 68, 120, 1), (1, 192, 128, 16, 24, 1)])
+def test_dwpw_fused_latent(B, Cin, Cout, H, W, epi):
+    _dwpw_case(B, Cin, Cout, H, W, epi)
+
+
+def _dwpw_case(B, Cn, Cout, H, W, epi):
     from mlic_amd import _lib
-    EPI_RES = 64
+    TANH, MASK_A, MASK_N, EPI_RES = 8, 16, 32, 64
     g = torch.Generator().manual_seed(5)
     dev = torch.device("cuda")
     x = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
     dw = ((torch.rand(Cn, 1, 3, 3, generator=g) - 0.5) * 0.6).to(dev)
     db = (torch.rand(Cn, generator=g) - 0.5).to(dev)
-    w = ((torch.rand(Cn, Cn, 1, 1, generator=g) - 0.5) * 0.2).to(dev)
-    b = (torch.rand(Cn, generator=g) - 0.5).to(dev)
-    res = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
+    w = ((torch.rand(Cout, Cn, 1, 1, generator=g) - 0.5) * 0.2).to(dev)
+    b = (torch.rand(Cout, generator=g) - 0.5).to(dev)
+    res = (torch.rand(B, Cout, H, W, generator=g) - 0.5).to(dev)
     st = torch.cuda.current_stream().cuda_stream
-    y = torch.full((B, Cn, H, W), float("nan"), device=dev)
+    y = torch.full((B, Cout, H, W), float("nan"), device=dev)
+    args = (C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()), C.c_void_p(db.data_ptr()),
+            C.c_void_p(w.data_ptr()), C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()), B, Cn, Cout, H, W, epi,
+            C.c_void_p(res.data_ptr()))
     if W % 2:  # a lane's pixel pair must be inside the row or outside it: the model runs these unfused
         with pytest.raises(_lib.MlicError):
-            _lib.call("mlic_dwpw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
-                      C.c_void_p(db.data_ptr()), C.c_void_p(w.data_ptr()), C.c_void_p(b.data_ptr()),
-                      C.c_void_p(y.data_ptr()), B, Cn, Cn, H, W, epi, C.c_void_p(res.data_ptr()))
+            _lib.call("mlic_dwpw_run", *args)
         return
-    _lib.call("mlic_dwpw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
-              C.c_void_p(db.data_ptr()), C.c_void_p(w.data_ptr()), C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()),
-              B, Cn, Cn, H, W, epi, C.c_void_p(res.data_ptr()))
+    _lib.call("mlic_dwpw_run", *args)
     t = torch.full((B, Cn, H, W), float("nan"), device=dev)
     _lib.call("mlic_dw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(dw.data_ptr()),
               C.c_void_p(db.data_ptr()), C.c_void_p(t.data_ptr()), B, Cn, H, W, 1, 0)
-    y2 = torch.full((B, Cn, H, W), float("nan"), device=dev)
+    y2 = torch.full((B, Cout, H, W), float("nan"), device=dev)
     _lib.call("mlic_conv_run", C.c_void_p(st), 3, C.c_void_p(t.data_ptr()), C.c_void_p(w.data_ptr()),
-              C.c_void_p(b.data_ptr()), C.c_void_p(y2.data_ptr()), B, Cn, Cn, H, W, 1, 1, epi, None,
+              C.c_void_p(b.data_ptr()), C.c_void_p(y2.data_ptr()), B, Cn, Cout, H, W, 1, 1, epi, None,
               C.c_void_p(res.data_ptr()))
     assert torch.equal(y, y2)
     ref = F.conv2d(F.conv2d(x.double(), dw.double(), db.double(), padding=1, groups=Cn), w.double(), b.double())
     if epi & 1:
         ref = F.gelu(ref)
+    if epi & TANH:
+        ref = 0.5 * torch.tanh(ref)
+    if epi & (MASK_A | MASK_N):  # checkerboard: anchor cells have (h + w) odd
+        hh = torch.arange(H, device=dev).view(-1, 1)
+        ww = torch.arange(W, device=dev).view(1, -1)
+        anchor = ((hh + ww) % 2) == 1
+        ref = ref * (anchor if epi & MASK_A else ~anchor).to(ref.dtype)
     if epi & EPI_RES:
         ref = ref + res.double()
     check(y, ref.float(), rtol=1e-6)
