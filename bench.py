@@ -375,7 +375,8 @@ def main():
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         max_per_rank = int(mx.item())
     allrec = mdist.gather_records(rec.to(dev), max_per_rank=max_per_rank).cpu()
-    assert allrec.shape[0] == n_jobs_total, (allrec.shape, n_jobs_total)
+    # every job of the list exactly once (emulated: this rank's share of it)
+    assert allrec.shape[0] == (len(jobs) if emulated else n_jobs_total), (allrec.shape, n_jobs_total)
 
     # live roofline: extra profiled (untimed) steps.  Pass 1 runs the timed steps' lane count, so its
     # per-launch averages are what rocprofv3 sees over the whole run (concurrent lanes stretch each
