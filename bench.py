@@ -70,7 +70,9 @@ WORKLOADS = {
                   desc="config 3: MLICPP_S compress+decompress of 1920x1088 images"),
     "sd1080": dict(model="MLICPP_M_SMALL_DEC", groups=[(1088, 1920, 32)], scaling="weak",
                    desc="config 3: MLICPP_M_SMALL_DEC compress+decompress of 1920x1088 images"),
-    "kodak-sweep": dict(model="MLICPP_L", scaling="strong",
+    # the sweep's 12 (rate, shape) batches of 4-20 Kodak-size images fill the GPU best as 6 concurrent
+    # batches of 2 lanes each (measured: 310 img/s vs 224 with 4 x 4, 194 with 6 x 4, 249 with 12 x 2)
+    "kodak-sweep": dict(model="MLICPP_L", scaling="strong", lanes=2, group_concurrency=6,
                         desc="config 4: MLICPP_L 24 Kodak-size images x 6 lambda stand-ins, LPT-sharded"),
     "vbr-mixed": dict(model="MLICPP_L_VBR", groups=[(2176, 3840, 2), (1088, 1920, 6)], scaling="weak",
                       desc="config 5: MLICPP_L_VBR 4K + 1080p batch, one VBR level per image"),
@@ -87,8 +89,9 @@ def parse():
     ap.add_argument("--rate", type=int, default=1,
                     help="realistic-rate weight set (0..5, synthetic.RATE_LAMBDAS) of fixed-rate workloads; "
                          "-1 = the round-1 high-rate set")
-    ap.add_argument("--lanes", type=int, default=int(os.environ.get("MLIC_LANES", "4")),
-                    help="host threads x HIP streams per GPU for compress/decompress")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="host threads x HIP streams per GPU for compress/decompress (0: the workload's "
+                         "default, else $MLIC_LANES or 4)")
     ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "2")),
                     help="dense-conv arithmetic: 2 = split-fp16 MFMA v2 + specialised kernels, "
                          "1 = f16x3 v1 tiles, 0 = fp32 MFMA")
@@ -104,14 +107,20 @@ def parse():
                          "steps' and rocprofv3's per-kernel averages; 1 = isolated per-kernel times)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
                     help="PMC-derived HBM bytes per launch of the dominant family (tools/pmc_traffic.py)")
-    ap.add_argument("--group-concurrency", type=int, default=4,
+    ap.add_argument("--group-concurrency", type=int, default=0,
                     help="(weights, shape) batches of a step run concurrently, each on its own model "
                          "instance, lanes and stream (1 = one after another)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="run rank --emulate-rank's share of a W-rank job list on this one GPU, with 1/W of "
                          "the host cores (a prediction of one rank of a W-GPU run; value = that rank's img/s)")
     ap.add_argument("--emulate-rank", type=int, default=0)
-    return ap.parse_args()
+    a = ap.parse_args()
+    wl = WORKLOADS[a.config]
+    if a.lanes <= 0:
+        a.lanes = int(os.environ["MLIC_LANES"]) if "MLIC_LANES" in os.environ else wl.get("lanes", 4)
+    if a.group_concurrency <= 0:
+        a.group_concurrency = wl.get("group_concurrency", 4)
+    return a
 
 
 # ------------------------------------------------------------------------------------------ jobs

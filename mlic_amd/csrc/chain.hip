@@ -45,20 +45,17 @@ __device__ __forceinline__ half8 chain_frag(const char* base, int row, int granu
   return *reinterpret_cast<const half8*>(base + row * 128 + ((granule ^ chswz(row)) << 4));
 }
 
-// hi/lo split of 8 values; bad: the fp16 range guard's per-lane bit (any |v| >= 65520, which rounds
-// to inf in fp16; a NaN propagates as on the fp32 path), pinned after every split (an asm operand) so
-// the compiler cannot sink the checks to the end of the kernel and keep every split value alive
-__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l, int& bad) {
-  float m = 0.0f;
+// hi/lo split of 8 values.  The fp16 range guard needs no check here: a value with |v| >= 65520 splits
+// to hi = +-inf (lo = -+inf or NaN), which makes every accumulator it reaches inf / NaN; GELU maps
+// inf to NaN, NaN propagates through every later layer's split and MFMAs, and the output store
+// checks that the chain's outputs are finite (one compare per output instead of a max per input)
+__device__ __forceinline__ void split8(const float (&v)[8], half8& h, half8& l) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    m = __builtin_fmaxf(m, __builtin_fabsf(v[e]));
     const _Float16 hv = (_Float16)v[e];
     h[e] = hv;
     l[e] = (_Float16)(v[e] - (float)hv);
   }
-  bad |= m >= 65520.0f ? 1 : 0;
-  asm volatile("" : "+v"(bad));
 }
 }  // namespace
 
@@ -223,7 +220,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     step_begin(t);
     half8 bh[2], bl[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) split8(f[j], bh[j], bl[j], bad);
+    for (int j = 0; j < 2; ++j) split8(f[j], bh[j], bl[j]);
     // keep the reload of f below its last use, so the ring slot stays in the same registers (an
     // overlap would make the register allocator rotate the ring with copies that wait for the loads)
     __builtin_amdgcn_sched_barrier(0);
@@ -259,7 +256,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     const float* bq = sbias + boff + 32 * c + 16 * q + 4 * G + e;
 #pragma unroll
     for (int k = 0; k < 2; ++k) v[j][4 * q + e + k] = gelu_erf(__builtin_fmaf(acc[2 * c + q][j][e + k], unscale, bq[k]));
-    if ((pi & 3) == 3) split8(v[j], oh[j], ol[j], bad);
+    if ((pi & 3) == 3) split8(v[j], oh[j], ol[j]);
   };
 
   // one layer fed from the previous layer's accumulators: NCH K-chunks, COUT rows, steps t0 .. t0 +
@@ -291,7 +288,6 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   // the output of the last layer: bias (+ residual), fp32 NCHW store
   auto store = [&](auto& acc, auto cout_c, int boff, int wexp) {
     constexpr int COUT = decltype(cout_c)::value;
-    range_report(P.rflag, bad != 0);
 #ifdef MLIC_CHAIN_TRACE
     if (tr_wg >= 0 && lane == 0) {
       CH_TR(T < CH_TR_STEPS ? T : CH_TR_STEPS - 1, 0);
@@ -310,10 +306,12 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
         for (int e = 0; e < 4; ++e) {
           const int co = 16 * i + 4 * G + e;
           float v = __builtin_fmaf(acc[i][j][e], unscale, sbias[boff + co]);
+          bad |= !(__builtin_fabsf(v) <= 3.4e38f) ? 1 : 0;
           if (P.res) v += P.res[(int64_t)b * P.res_bs + (int64_t)co * HW + px];
           P.out[(int64_t)b * P.out_bs + (int64_t)co * HW + px] = v;
         }
       }
+    range_report(P.rflag, bad != 0);
   };
 
   floatx4 acc1[C2 / 16][2];

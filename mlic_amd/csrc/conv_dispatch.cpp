@@ -47,8 +47,10 @@ int conv_select(const ConvParams& P, const ConvWeights& w, int precision) {
   // 1080p and Kodak-size latents, the activation pack included).  Any grid: the split-K path
   // (x4_splitk) fills the chip for few-tile 3x3 / 5x5 shapes (h_s at the z grid, 8 x 12 .. 17 x 30:
   // 1.5-2.5x x3v2)
+  // Round 3: 3x3 convs from Cout 64 too (the small-decoder model's dense channel-context convs
+  // 96..288 -> 96 / 128 at the latent grid: 1.26-1.75x x3v2)
   const bool big1 = (int64_t)P.Cin * P.Cout >= (1 << 18), mid1 = P.Cin >= 192 && P.Cout >= 192;
-  const bool x4_shape = P.K == 1 ? (big1 || mid1) : P.Cout >= (P.K == 3 ? 192 : 64);
+  const bool x4_shape = P.K == 1 ? (big1 || mid1) : P.Cout >= 64;
   if (w.wx4 && x4_on() && x4_k_on(P.K) && x4_shape && conv_x4_ok(P, w.cin_pad)) return CONV_X4;
   // halo: the 5x5 reprojection (145 vs 126 TF/s); for 3x3 the 8-wave 256x256 x3v2 tile is faster
   // (243 vs 232 TF/s on the g_s subpel conv), for 1x1 the halo staging does not pay

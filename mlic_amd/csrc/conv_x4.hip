@@ -69,9 +69,13 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
                                                       const _Float16* __restrict__ wx, int nchunk, int H, int W,
                                                       int abl, int nsplit) {
   constexpr int KK = K * K;
-  constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
+  // BM 256 / 128 / 64: 64 Cout rows per wave (4 fragments); BM 192 (Cout 129..192, e.g. the
+  // small-decoder model's dense 192 -> 192 convs, which waste a quarter of a 256-row tile): 4 x 2
+  // waves of 48 rows (3 fragments) x 128 pixels
+  constexpr int WAVES_M = BM == 192 ? 4 : BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WN = BN / WAVES_N;        // pixels per wave
-  constexpr int TM = 4, TN = WN / 16;     // 16x16 fragments per wave
+  constexpr int TM = BM / (16 * WAVES_M), TN = WN / 16;  // 16x16 fragments per wave
+  constexpr int WR = 16 * TM;             // Cout rows per wave
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
   constexpr int NAB = RS ? 2 : 3;  // A ring slots
   constexpr int B_OFF = NAB * A_BYTES, LDS = NAB * A_BYTES + 2 * B_BYTES;
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       half8 ah[TM], al[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int row = wm * 64 + i * 16 + l16;
+        const int row = wm * WR + i * 16 + l16;
         ah[i] = lds_frag(As, row, G);
         al[i] = lds_frag(As, row, G + 4);
       }
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     half8 ah[TM], al[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int row = wm * 64 + i * 16 + l16;
+      const int row = wm * WR + i * 16 + l16;
       ah[i] = lds_frag(As, row, G);
       al[i] = lds_frag(As, row, G + 4);
     }
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     return;
   }
   float* ep = reinterpret_cast<float*>(sm) + wave * 16 * EP;
-  const int co_w = ct * BM + wm * 64;
+  const int co_w = ct * BM + wm * WR;
   const bool shuf = (P.epi & EPI_SHUFFLE) != 0;
   const bool vec = conv_vec_ok(P) && !(shuf && (P.epi & (EPI_GDN | EPI_IGDN | EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR)));
 #pragma unroll
@@ -456,6 +460,7 @@ __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _F
 // 256-row Cout tiles unless 128-row tiles pad at least 1/8 of Cout less (e.g. 320, 640 -> 128)
 int x4_bm(int Cout) {
   if (Cout <= 64) return 64;
+  if (Cout > 128 && Cout <= 192) return 192;
   const int w256 = (Cout + 255) / 256 * 256 - Cout, w128 = (Cout + 127) / 128 * 128 - Cout;
   return (Cout >= 192 && 8 * (w256 - w128) <= Cout) ? 256 : 128;
 }
@@ -562,8 +567,11 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
   else if (x4_rs())
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
                        nsplit);
-  else
+  else if constexpr (BM != 192)  // (the DMA path's counted waits assume 1, 2 or 4 A pieces per wave)
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, false, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, 1);
+  else
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
+                       nsplit);
   HIP_OK(hipGetLastError());
 }
 
@@ -612,6 +620,7 @@ void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* w
   }
 #define MLIC_X4_BM(K)                                                  \
   (bm == 256 ? launch_x4<K, 256>(R, act, wx, nchunk, st, nsplit, hi)       \
+   : bm == 192 ? launch_x4<K, 192>(R, act, wx, nchunk, st, nsplit, hi)     \
    : bm == 128 ? launch_x4<K, 128>(R, act, wx, nchunk, st, nsplit, hi)     \
                : launch_x4<K, 64>(R, act, wx, nchunk, st, nsplit, hi))
   switch (P.K) {

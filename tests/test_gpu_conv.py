@@ -173,6 +173,9 @@ def test_halo_k1_k5(shape):
     (1, 480, 1920, 8, 16, 3, SHUFFLE | GELU),   # h_s subpel 480 -> 1920, 8 Cout tiles
     (2, 800, 64, 17, 30, 1, RES),               # 64-row tile (LocalContext fusion), residual
     (1, 128, 40, 9, 37, 1, 0),                  # Cout < 64, ragged folded pixel row
+    (2, 192, 192, 24, 40, 3, GELU),             # 192-row tile (4 x 2 waves of 48 rows): SD dense g_a conv
+    (1, 96, 160, 19, 45, 3, RES),               # 192-row tile, 160 rows real, ragged pixel tiles
+    (2, 192, 192, 16, 32, 3, GDN | SQUARE | RES),  # 192-row tile, GDN epilogue + residual
 ])
 def test_x4(shape):
     B, cin, cout, H, W, K, epi = shape
@@ -202,6 +205,7 @@ def _fp16_operands(x, w):
     (1, 96, 384, 16, 40, 3, SHUFFLE | GELU),    # MLICPP_S width: 96 channels = one zero-padded chunk pair
     (1, 100, 200, 9, 33, 3, RES),               # Cin not a multiple of 32, partial Cout tile, residual
     (1, 320, 64, 13, 37, 5, 0),                 # 5x5 with few tiles: the split-K path
+    (1, 192, 192, 16, 40, 3, GELU),             # 192-row tile
 ])
 def test_x4_fp16_operands(shape):
     """The reduced-precision synthesis form: fp16 x fp16 products with fp32 accumulation.

@@ -164,7 +164,7 @@ def test_pmf_to_quantized_cdf_properties():
 
 
 def test_conv_choice_pins_the_measured_selection():
-    """The kernel family per layer shape that round 2's A/B measurements chose; a
+    """The kernel family per layer shape that the A/B measurements chose; a
     regression here changes speed (and, as families round differently, the exact bits)."""
     F32, X3, X3V2, PW, NARROW, SMALLCIN, HALO, X4 = range(8)
     impl = C.c_int()
@@ -185,6 +185,8 @@ def test_conv_choice_pins_the_measured_selection():
     assert choice(640, 6400, 68, 120, 1) == X4            # hoisted EntropyParameters GEMM
     assert choice(288, 96, 68, 120, 5) == X4              # 5x5 reprojections
     assert choice(192, 192, 544, 960, 3, stride=2) == X4  # small-decoder dense strided conv
+    assert choice(96, 128, 68, 120, 3) == X4              # small-decoder channel context: 1.4x x3v2
+    assert choice(288, 96, 68, 120, 3, epi=1) == X4       # 1.5x
     assert choice(3, 192, 1088, 1920, 3, stride=2) == SMALLCIN
     assert choice(3, 192, 1088, 1920, 1, stride=2) == SMALLCIN
     assert choice(192, 12, 544, 960, 3) == NARROW
