@@ -165,17 +165,8 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       for (int i = 0; i < NA; ++i)
         *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave * NA + i) * 1024 + lane * 16) = ra[i];
     };
-    gload(s0);
-    lstore(s0);
-    if (s0 + 1 < s1) gload(s0 + 1);
-    for (int s = s0; s < s1; ++s) {
-      // this wave's stores of step s done; barrier: every wave's too, and step s-1's reads of the
-      // other slot are finished
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (s + 1 < s1) lstore(s + 1);
-      if (s + 2 < s1) gload(s + 2);
+    // step s's MFMAs on LDS slot s & 1 (fragment reads one pixel group ahead)
+    auto mfma_step = [&](int s) {
       const char* As = sm + (s & 1) * A_BYTES;
       const char* Bs = sm + B_OFF + (s & 1) * B_BYTES;
       half8 ah[TM], al[TM];
@@ -214,6 +205,19 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
         }
       }
+    };
+    gload(s0);
+    lstore(s0);
+    if (s0 + 1 < s1) gload(s0 + 1);
+    for (int s = s0; s < s1; ++s) {
+      // this wave's stores of step s done; barrier: every wave's too, and step s-1's reads of the
+      // other slot are finished
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 1 < s1) lstore(s + 1);
+      if (s + 2 < s1) gload(s + 2);
+      mfma_step(s);
     }
   } else {
   static_assert(!HI, "the reduced-precision form runs on the register-staged path");
