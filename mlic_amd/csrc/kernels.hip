@@ -417,6 +417,9 @@ void local_attn_valu(const LocalAttnParams& P, hipStream_t st) {
 // kmask = 1: only anchor positions are keys (the intra-slice squeezed anchor half); qmask = 1: only
 // non-anchor positions have queries (outputs 0 at anchors).
 constexpr int CTX_CHUNK = 64;
+#ifndef MLIC_LINATT_ABL  // diagnostics build: 1 = no K.V^T accumulation, 2 = no ctx^T.q contraction
+#define MLIC_LINATT_ABL 0
+#endif
 
 // record per (image, head, split): [HD] key maxima m_s, [HD][HD] sum_p exp(k_c - m_s) v_d,
 // [HD] sum_p exp(k_c - m_s).  256 threads; the K.V^T tile of thread t is a TC x TC block
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(256) void ctx_partial_kernel(const float* __restric
     }
     __syncthreads();
 #pragma unroll 8
-    for (int pp = 0; pp < CTX_CHUNK; ++pp) {
+    for (int pp = 0; pp < ((MLIC_LINATT_ABL & 1) ? 1 : CTX_CHUNK); ++pp) {  // (diagnostics: no K.V^T FLOPs)
       if constexpr (TC == 2) {
         const float2 a = *reinterpret_cast<const float2*>(&kt[pp][c0]);
         const float2 v = *reinterpret_cast<const float2*>(&vt[pp][d0]);
@@ -569,7 +572,7 @@ __global__ __launch_bounds__(256) void attn_apply_kernel(const float* __restrict
 #pragma unroll
   for (int d = 0; d < hd; ++d) a[d] = 0.0f;
 #pragma unroll
-  for (int c = 0; c < hd; ++c) {
+  for (int c = 0; c < ((MLIC_LINATT_ABL & 2) ? 1 : hd); ++c) {  // (diagnostics: no ctx^T.q FLOPs)
 #pragma unroll
     for (int d4 = 0; d4 < hd / 4; ++d4) {
       const float4 w = *reinterpret_cast<const float4*>(&cs[c * hd + 4 * d4]);  // broadcast
