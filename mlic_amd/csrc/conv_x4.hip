@@ -71,8 +71,9 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   constexpr int KK = K * K;
   // BM 256 / 128 / 64: 64 Cout rows per wave (4 fragments); BM 192 (Cout 129..192, e.g. the
   // small-decoder model's dense 192 -> 192 convs, which waste a quarter of a 256-row tile): 4 x 2
-  // waves of 48 rows (3 fragments) x 128 pixels
-  constexpr int WAVES_M = BM == 192 ? 4 : BM / 64, WAVES_N = 8 / WAVES_M;
+  // waves of 48 rows (3 fragments) x 128 pixels; BM 96 (Cout 65..96: the context reprojections'
+  // 96 outputs): 2 x 4 waves of 48 rows x 64 pixels
+  constexpr int WAVES_M = BM == 192 ? 4 : BM == 96 ? 2 : BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WN = BN / WAVES_N;        // pixels per wave
   constexpr int TM = BM / (16 * WAVES_M), TN = WN / 16;  // 16x16 fragments per wave
   constexpr int WR = 16 * TM;             // Cout rows per wave
@@ -147,7 +148,11 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   const int G = lane >> 4, l16 = lane & 15;
   if constexpr (RS) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 rb[NB], ra[NA];
+    // A pieces (1 KB = 8 rows of the step's image) dealt round-robin over the 8 waves: piece
+    // wave + 8 i (BM 96 has 12: waves 0-3 take two)
+    constexpr int NPA = A_BYTES / 1024, NAR = (NPA + 7) / 8;
+    const _Float16* asrc_rs = wx + ((int64_t)ct * nsteps * BM) * ROWH + wave * 512 + lane * 8;
+    u32x4 rb[NB], ra[NAR];
     auto gload = [&](int st) {  // step st's pieces of this wave -> registers
       const int cc = st / KK, tap = st - cc * KK;
       const int ky = tap / K, kx = tap - ky * K;
@@ -155,15 +160,18 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
 #pragma unroll
       for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const u32x4*>(bsrc[i] + d);
 #pragma unroll
-      for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const u32x4*>(asrc + (int64_t)st * BM * ROWH + i * 512);
+      for (int i = 0; i < NAR; ++i)
+        if (NPA % 8 == 0 || wave + 8 * i < NPA)
+          ra[i] = *reinterpret_cast<const u32x4*>(asrc_rs + (int64_t)st * BM * ROWH + i * 8 * 512);
     };
     auto lstore = [&](int st) {  // registers -> the LDS slot of step st (the DMA's lane-linear image)
 #pragma unroll
       for (int i = 0; i < NB; ++i)
         *reinterpret_cast<u32x4*>(sm + B_OFF + (st & 1) * B_BYTES + (wave * NB + i) * 1024 + lane * 16) = rb[i];
 #pragma unroll
-      for (int i = 0; i < NA; ++i)
-        *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave * NA + i) * 1024 + lane * 16) = ra[i];
+      for (int i = 0; i < NAR; ++i)
+        if (NPA % 8 == 0 || wave + 8 * i < NPA)
+          *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave + 8 * i) * 1024 + lane * 16) = ra[i];
     };
     // step s's MFMAs on LDS slot s & 1 (fragment reads one pixel group ahead)
     auto mfma_step = [&](int s) {
@@ -464,6 +472,7 @@ __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _F
 // 256-row Cout tiles unless 128-row tiles pad at least 1/8 of Cout less (e.g. 320, 640 -> 128)
 int x4_bm(int Cout) {
   if (Cout <= 64) return 64;
+  if (Cout > 64 && Cout <= 96) return 96;
   if (Cout > 128 && Cout <= 192) return 192;
   const int w256 = (Cout + 255) / 256 * 256 - Cout, w128 = (Cout + 127) / 128 * 128 - Cout;
   return (Cout >= 192 && 8 * (w256 - w128) <= Cout) ? 256 : 128;
@@ -571,7 +580,7 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
   else if (x4_rs())
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
                        nsplit);
-  else if constexpr (BM != 192)  // (the DMA path's counted waits assume 1, 2 or 4 A pieces per wave)
+  else if constexpr (BM != 192 && BM != 96)  // (the DMA path's counted waits assume 1, 2 or 4 A pieces per wave)
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, false, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, 1);
   else
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
@@ -625,6 +634,7 @@ void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* w
 #define MLIC_X4_BM(K)                                                  \
   (bm == 256 ? launch_x4<K, 256>(R, act, wx, nchunk, st, nsplit, hi)       \
    : bm == 192 ? launch_x4<K, 192>(R, act, wx, nchunk, st, nsplit, hi)     \
+   : bm == 96 ? launch_x4<K, 96>(R, act, wx, nchunk, st, nsplit, hi)       \
    : bm == 128 ? launch_x4<K, 128>(R, act, wx, nchunk, st, nsplit, hi)     \
                : launch_x4<K, 64>(R, act, wx, nchunk, st, nsplit, hi))
   switch (P.K) {

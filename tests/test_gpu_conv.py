@@ -176,6 +176,9 @@ def test_halo_k1_k5(shape):
     (2, 192, 192, 24, 40, 3, GELU),             # 192-row tile (4 x 2 waves of 48 rows): SD dense g_a conv
     (1, 96, 160, 19, 45, 3, RES),               # 192-row tile, 160 rows real, ragged pixel tiles
     (2, 192, 192, 16, 32, 3, GDN | SQUARE | RES),  # 192-row tile, GDN epilogue + residual
+    (2, 256, 96, 17, 30, 5, 0),                 # 96-row tile (2 x 4 waves of 48 rows): context reprojection
+    (2, 160, 80, 17, 30, 3, GELU | RES),        # 96-row tile, 80 rows real
+    (1, 96, 96, 9, 45, 1, 0),                   # 96-row tile, 1x1, ragged folded pixel row
 ])
 def test_x4(shape):
     B, cin, cout, H, W, K, epi = shape
