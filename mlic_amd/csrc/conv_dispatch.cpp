@@ -81,7 +81,8 @@ int64_t conv_ws_bytes(int impl, const ConvParams& P, const ConvWeights& w) {
   // x4: the packed activations, then (256-byte aligned) the split-K partial planes
   if (impl != CONV_X4 && impl != CONV_X4H) return 0;
   const bool hi = impl == CONV_X4H;
-  return (2 * x4_act_halves(P, w.cin_pad, hi) + 255) / 256 * 256 + x4_part_bytes(P, w.cin_pad, hi);
+  const int64_t act = x4_direct_ok(P, hi) ? 0 : (2 * x4_act_halves(P, w.cin_pad, hi) + 255) / 256 * 256;
+  return act + x4_part_bytes(P, w.cin_pad, hi);
 }
 
 void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t st, void* ws) {
@@ -103,12 +104,13 @@ void conv_run(int impl, const ConvParams& P0, const ConvWeights& w, hipStream_t 
     case CONV_X4H: {
       const bool hi = impl == CONV_X4H;
       const _Float16* wx = hi ? w.wx4h : w.wx4;
-      MLIC_CHECK(ws && wx, "conv_x4: workspace and packed weights required");
-      _Float16* act = static_cast<_Float16*>(ws);
-      const int64_t abytes = (2 * x4_act_halves(P, w.cin_pad, hi) + 255) / 256 * 256;
+      const bool direct = x4_direct_ok(P, hi);  // 1x1: B rows built from the fp32 input in the kernel
+      MLIC_CHECK((ws || direct) && wx, "conv_x4: workspace and packed weights required");
+      _Float16* act = direct ? nullptr : static_cast<_Float16*>(ws);
+      const int64_t abytes = direct ? 0 : (2 * x4_act_halves(P, w.cin_pad, hi) + 255) / 256 * 256;
       float* part = x4_part_bytes(P, w.cin_pad, hi) > 0 ? reinterpret_cast<float*>(static_cast<char*>(ws) + abytes)
                                                          : nullptr;
-      x4_pack_act(P, w.cin_pad, act, st, hi);
+      if (!direct) x4_pack_act(P, w.cin_pad, act, st, hi);
       conv_x4_forward(P, act, wx, w.cin_pad, st, part, hi);
       break;
     }

@@ -64,7 +64,10 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 // HI: the reduced-precision form (g_s only): rows hold the fp16 value of 64 channels
 // (granules 0-3: channels 0-31 of the chunk, 4-7: channels 32-63) and a K-step is 2 MFMAs per
 // fragment pair covering 64 channels: fp16 x fp16 products, fp32 accumulation
-template <int K, int BM, bool RS, bool HI>
+// DIR (K = 1, split form): no packed copy -- the B rows are built from the fp32 NCHW input segments
+// in registers (lane = pixel, 16 channels per thread, split hi / lo with the pack kernel's RNE
+// conversions) and written into the same swizzled LDS image; the fp16 range check rides along
+template <int K, int BM, bool RS, bool HI, bool DIR = false>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
                                                       const _Float16* __restrict__ wx, int nchunk, int H, int W,
                                                       int abl, int nsplit) {
@@ -72,8 +75,9 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   // BM 256 / 128 / 64: 64 Cout rows per wave (4 fragments); BM 192 (Cout 129..192, e.g. the
   // small-decoder model's dense 192 -> 192 convs, which waste a quarter of a 256-row tile): 4 x 2
   // waves of 48 rows (3 fragments) x 128 pixels; BM 96 (Cout 65..96: the context reprojections'
-  // 96 outputs): 2 x 4 waves of 48 rows x 64 pixels
-  constexpr int WAVES_M = BM == 192 ? 4 : BM == 96 ? 2 : BM / 64, WAVES_N = 8 / WAVES_M;
+  // 96 outputs): 2 x 4 waves of 48 rows x 64 pixels; BM 224 (Cout 193..224: the LRP's and the
+  // context's 224-channel 1x1s): 2 x 4 waves of 112 rows (7 fragments) x 64 pixels
+  constexpr int WAVES_M = BM == 192 ? 4 : (BM == 96 || BM == 224) ? 2 : BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WN = BN / WAVES_N;        // pixels per wave
   constexpr int TM = BM / (16 * WAVES_M), TN = WN / 16;  // 16x16 fragments per wave
   constexpr int WR = 16 * TM;             // Cout rows per wave
@@ -152,22 +156,84 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     // wave + 8 i (BM 96 has 12: waves 0-3 take two)
     constexpr int NPA = A_BYTES / 1024, NAR = (NPA + 7) / 8;
     const _Float16* asrc_rs = wx + ((int64_t)ct * nsteps * BM) * ROWH + wave * 512 + lane * 8;
-    u32x4 rb[NB], ra[NAR];
-    auto gload = [&](int st) {  // step st's pieces of this wave -> registers
+    u32x4 rb[DIR ? 1 : NB], ra[NAR];
+    // DIR: tile pixel dn = 64 (wave & 3) + lane (flat pixel dp, clamped into the image: the ragged
+    // tail's outputs are discarded), channels dch .. dch + 15 of the step's 32-channel chunk
+    float rv[DIR ? 16 : 1];
+    const int dn = (wave & 3) * 64 + lane, dch = (wave >> 2) * 16;
+    const int dp = min(oy0 * TC + dn, npix - 1);
+    uint32_t dmax = 0;  // max |bits| of every input value this thread split (the fp16 range check)
+    auto gload = [&](int st) __attribute__((always_inline)) {  // step st's pieces of this wave -> registers
       const int cc = st / KK, tap = st - cc * KK;
       const int ky = tap / K, kx = tap - ky * K;
-      const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
+      if constexpr (DIR) {
+        // 16-aligned 16-channel groups never straddle a segment (conv_x4_ok)
+        const int ch0 = cc * 32 + dch;
+        // (compile-time segment indices: a runtime index into P would copy it to scratch)
+        const float* sp = P.seg[0].p;
+        int64_t sbs = P.seg[0].bs;
+        int c0 = 0, cend = 0;
 #pragma unroll
-      for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const u32x4*>(bsrc[i] + d);
+        for (int k = 1; k < MAXSEG; ++k) {
+          cend += P.seg[k - 1].C;
+          // (opaque copies: a select between two loads of P would become a load from a selected
+          // address into P, which also sends P to scratch)
+          uint64_t pk = (uint64_t)P.seg[k].p, bk = (uint64_t)P.seg[k].bs;
+          asm("" : "+s"(pk), "+s"(bk));
+          if (k < P.nseg && ch0 >= cend) {
+            sp = (const float*)pk;
+            sbs = (int64_t)bk;
+            c0 = cend;
+          }
+        }
+        typedef const __attribute__((address_space(1))) float gfloat;
+        gfloat* src = (gfloat*)(sp + (int64_t)b * sbs + (int64_t)(ch0 - c0) * npix) + dp;
+        const int nval = P.Cin - ch0;
+        if (nval >= 16) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) rv[j] = src[(int64_t)j * npix];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) rv[j] = j < nval ? src[(int64_t)j * npix] : 0.0f;
+        }
+      } else {
+        const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const u32x4*>(bsrc[i] + d);
+      }
 #pragma unroll
       for (int i = 0; i < NAR; ++i)
         if (NPA % 8 == 0 || wave + 8 * i < NPA)
           ra[i] = *reinterpret_cast<const u32x4*>(asrc_rs + (int64_t)st * BM * ROWH + i * 8 * 512);
     };
-    auto lstore = [&](int st) {  // registers -> the LDS slot of step st (the DMA's lane-linear image)
+    auto lstore = [&](int st) __attribute__((always_inline)) {  // registers -> the LDS slot of step st (the DMA's lane-linear image)
+      if constexpr (DIR) {
+        typedef float float2v __attribute__((ext_vector_type(2)));
+        typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+        char* row = sm + B_OFF + (st & 1) * B_BYTES + dn * ROWB;
+        const int sw = swz(dn), g0 = dch / 8;  // logical granules g0, g0 + 1 (hi), g0 + 4, g0 + 5 (lo)
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
-        *reinterpret_cast<u32x4*>(sm + B_OFF + (st & 1) * B_BYTES + (wave * NB + i) * 1024 + lane * 16) = rb[i];
+        for (int q = 0; q < 2; ++q) {
+          half8 h, l;
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const float2v v = {rv[8 * q + j], rv[8 * q + j + 1]};
+            const half2v hv = __builtin_convertvector(v, half2v);
+            const half2v lv = __builtin_convertvector(v - __builtin_convertvector(hv, float2v), half2v);
+            h[j] = hv[0];
+            h[j + 1] = hv[1];
+            l[j] = lv[0];
+            l[j + 1] = lv[1];
+            dmax = max(dmax, max(__float_as_uint(v[0]) & 0x7fffffffu, __float_as_uint(v[1]) & 0x7fffffffu));
+          }
+          *reinterpret_cast<half8*>(row + (((g0 + q) ^ sw) << 4)) = h;
+          *reinterpret_cast<half8*>(row + (((g0 + q + 4) ^ sw) << 4)) = l;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          *reinterpret_cast<u32x4*>(sm + B_OFF + (st & 1) * B_BYTES + (wave * NB + i) * 1024 + lane * 16) = rb[i];
+      }
 #pragma unroll
       for (int i = 0; i < NAR; ++i)
         if (NPA % 8 == 0 || wave + 8 * i < NPA)
@@ -227,6 +293,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       if (s + 2 < s1) gload(s + 2);
       mfma_step(s);
     }
+    if constexpr (DIR) range_report(P.rflag, f16_unsafe(__uint_as_float(dmax)));
   } else {
   static_assert(!HI, "the reduced-precision form runs on the register-staged path");
   // issue order: A0 B0 A1 | step 0: B1 A2 | step 1: B2 A3 | ...  Every step issues its NG DMA
@@ -474,6 +541,11 @@ int x4_bm(int Cout) {
   if (Cout <= 64) return 64;
   if (Cout > 64 && Cout <= 96) return 96;
   if (Cout > 128 && Cout <= 192) return 192;
+  static const bool t224 = [] {  // A/B: MLIC_X4_BM224=0 keeps 256-row tiles for Cout 193..224
+    const char* e = std::getenv("MLIC_X4_BM224");
+    return !(e && e[0] == '0');
+  }();
+  if (t224 && Cout > 192 && Cout <= 224) return 224;
   const int w256 = (Cout + 255) / 256 * 256 - Cout, w128 = (Cout + 127) / 128 * 128 - Cout;
   return (Cout >= 192 && 8 * (w256 - w128) <= Cout) ? 256 : 128;
 }
@@ -563,6 +635,15 @@ static bool x4_rs() {
   return on;
 }
 
+// $MLIC_X4_DIRECT=0: 1x1 layers read the packed copy too (A/B switch)
+bool x4_direct_ok(const ConvParams& P, bool hi) {
+  static const bool on = [] {
+    const char* e = std::getenv("MLIC_X4_DIRECT");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && P.K == 1 && !hi && !(P.epi & EPI_SQUARE_IN) && x4_rs();
+}
+
 template <int K, int BM>
 static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* wx, int nchunk, hipStream_t st,
                       int nsplit, bool hi) {
@@ -574,13 +655,16 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
     const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
     return e ? std::atoi(e) : 0;
   }();
-  if (hi)
+  if (K == 1 && !act)
+    hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false, K == 1>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W,
+                       abl, nsplit);
+  else if (hi)
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
                        nsplit);
   else if (x4_rs())
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
                        nsplit);
-  else if constexpr (BM != 192 && BM != 96)  // (the DMA path's counted waits assume 1, 2 or 4 A pieces per wave)
+  else if constexpr (BM != 192 && BM != 96 && BM != 224)  // (the DMA path's counted waits: 1, 2 or 4 A pieces per wave)
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, false, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl, 1);
   else
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
@@ -613,10 +697,11 @@ int64_t x4_part_bytes(const ConvParams& P, int cin_pad, bool hi) {
 
 void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* wx, int cin_pad, hipStream_t st,
                      float* part, bool hi) {
-  MLIC_CHECK(conv_x4_ok(P, cin_pad) && act && wx, "conv_x4: unsupported shape");
-  // the ConvParams input segments are not read: the packed copy (x4_pack_act) is
+  // act == nullptr: the direct form (x4_direct_ok), which reads the ConvParams input segments;
+  // otherwise they are not read: the packed copy (x4_pack_act) is
+  MLIC_CHECK(conv_x4_ok(P, cin_pad) && wx && (act || x4_direct_ok(P, hi)), "conv_x4: unsupported shape");
   ConvParams Q = P;
-  Q.epi &= ~EPI_SQUARE_IN;
+  if (act) Q.epi &= ~EPI_SQUARE_IN;
   const int nchunk = x4_nchunk(cin_pad, hi);
   const int bm = x4_bm(P.Cout);
   const int nsplit = part ? x4_splitk(P, cin_pad, hi) : 1;
@@ -635,6 +720,7 @@ void conv_x4_forward(const ConvParams& P, const _Float16* act, const _Float16* w
   (bm == 256 ? launch_x4<K, 256>(R, act, wx, nchunk, st, nsplit, hi)       \
    : bm == 192 ? launch_x4<K, 192>(R, act, wx, nchunk, st, nsplit, hi)     \
    : bm == 96 ? launch_x4<K, 96>(R, act, wx, nchunk, st, nsplit, hi)       \
+   : bm == 224 ? launch_x4<K, 224>(R, act, wx, nchunk, st, nsplit, hi)     \
    : bm == 128 ? launch_x4<K, 128>(R, act, wx, nchunk, st, nsplit, hi)     \
                : launch_x4<K, 64>(R, act, wx, nchunk, st, nsplit, hi))
   switch (P.K) {

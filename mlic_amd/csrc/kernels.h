@@ -55,6 +55,8 @@ void x4_pack_weights(const _Float16* wh, const _Float16* wl, int Cout, int KK, i
 int64_t x4_act_halves(const ConvParams& P, int cin_pad, bool hi = false);
 bool conv_x4_ok(const ConvParams& P, int cin_pad);
 void x4_pack_act(const ConvParams& P, int cin_pad, _Float16* dst, hipStream_t st, bool hi = false);
+// 1x1 layers: x4 builds its B rows from the fp32 input itself (no packed copy; act = nullptr)
+bool x4_direct_ok(const ConvParams& P, bool hi);
 // part: the split-K partial planes (x4_part_bytes bytes; nullptr = no split)
 int x4_splitk(const ConvParams& P, int cin_pad, bool hi = false);
 int64_t x4_part_bytes(const ConvParams& P, int cin_pad, bool hi = false);

@@ -557,7 +557,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
   // the reduced-precision form when requested (set_synthesis_precision(1)) and both images exist
   const bool hi = gs_fp16_ && w1.wx4h && w2.wx4h;
   const size_t m = L().arena.mark();
-  _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((conv_ws_bytes(hi ? CONV_X4H : CONV_X4, P1, c1) + 3) / 4));
+  _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((2 * x4_act_halves(P1, w1.cin_pad, hi) + 3) / 4));
   timed(PCAT_ELEM, 0.0, (hi ? 6.0 : 8.0) * L().B * P1.Cin * P1.H * P1.W,
         [&] { x4_pack_act(P1, w1.cin_pad, act, L().st, hi); }, w1.name + ".__x4_pack");
   run_conv(P1, w1, act, hi);

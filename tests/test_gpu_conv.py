@@ -179,10 +179,46 @@ def test_halo_k1_k5(shape):
     (2, 256, 96, 17, 30, 5, 0),                 # 96-row tile (2 x 4 waves of 48 rows): context reprojection
     (2, 160, 80, 17, 30, 3, GELU | RES),        # 96-row tile, 80 rows real
     (1, 96, 96, 9, 45, 1, 0),                   # 96-row tile, 1x1, ragged folded pixel row
+    (2, 640, 224, 17, 30, 1, GELU),             # 224-row tile (2 x 4 waves of 112 rows): LRP point conv
+    (1, 224, 200, 9, 33, 3, RES),               # 224-row tile, 200 rows real
 ])
 def test_x4(shape):
     B, cin, cout, H, W, K, epi = shape
     check(*run(X4, B, cin, cout, H, W, K, epi=epi))
+
+
+def _conv_raw(impl, x, w, b, epi):
+    from mlic_amd import _lib
+    B, Cin, H, W = x.shape
+    y = torch.full((B, w.shape[0], H, W), float("nan"), device=x.device)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("mlic_conv_run", C.c_void_p(st), impl, C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()),
+              C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()), B, Cin, w.shape[0], H, W, 1, 1, epi, None, None)
+    torch.cuda.synchronize()
+    return y
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 640, 224, 17, 30),   # LRP point conv, 224-row tile
+    (2, 960, 320, 17, 30),   # entropy-parameters GEMM, 2 Cout tiles
+    (1, 100, 200, 9, 33),    # Cin 100: the last chunk's channels 96..99 real, the rest zeros
+    (1, 70, 64, 5, 7),       # Cin 70: one 16-channel group ragged, one all zeros; 35 px: one ragged tile
+    (2, 96, 96, 13, 37),     # 96-row tile
+])
+def test_x4_1x1_direct_vs_packed(shape):
+    """1x1 layers: x4 builds the split B rows from the fp32 input itself (no packed copy); under SQUARE
+    the pack kernel forms x^2 and the packed path runs.  Both multiply the same split operands in the
+    same order, so conv(x, SQUARE) == conv(x * x) bit for bit, and both match float64."""
+    B, cin, cout, H, W = shape
+    g = torch.Generator().manual_seed(7)
+    dev = torch.device("cuda")
+    x = (torch.rand(B, cin, H, W, generator=g) - 0.5).to(dev)
+    w = ((torch.rand(cout, cin, 1, 1, generator=g) - 0.5) / cin ** 0.5).to(dev)
+    b = (torch.rand(cout, generator=g) - 0.5).to(dev)
+    y_direct = _conv_raw(X4, x * x, w, b, 0)
+    y_packed = _conv_raw(X4, x, w, b, SQUARE)
+    assert torch.equal(y_direct, y_packed)
+    check(y_direct, F.conv2d((x * x).double(), w.double(), b.double()).float())
 
 
 @pytest.mark.parametrize("shape", [
