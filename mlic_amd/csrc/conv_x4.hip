@@ -539,7 +539,11 @@ __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _F
 // 256-row Cout tiles unless 128-row tiles pad at least 1/8 of Cout less (e.g. 320, 640 -> 128)
 int x4_bm(int Cout) {
   if (Cout <= 64) return 64;
-  if (Cout > 64 && Cout <= 96) return 96;
+  static const bool t96 = [] {  // A/B: MLIC_X4_BM96=0 keeps 128-row tiles for Cout 65..96
+    const char* e = std::getenv("MLIC_X4_BM96");
+    return !(e && e[0] == '0');
+  }();
+  if (t96 && Cout > 64 && Cout <= 96) return 96;
   if (Cout > 128 && Cout <= 192) return 192;
   static const bool t224 = [] {  // A/B: MLIC_X4_BM224=0 keeps 256-row tiles for Cout 193..224
     const char* e = std::getenv("MLIC_X4_BM224");
