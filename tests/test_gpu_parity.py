@@ -429,9 +429,22 @@ def test_vbr_mixed_levels_batch_equals_per_image():
     f = net(x, stage=2, s=levels)
     c = net.compress(x, stage=2, s=levels)
     d = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
-    dd = (d["x_hat"] - f["x_hat"]).abs()
-    assert torch.equal(d["x_hat"], f["x_hat"]), (int((dd > 0).sum()), float(dd.max()),
-                                                  [int((dd[i] > 0).sum()) for i in range(dd.shape[0])])
+    if not torch.equal(d["x_hat"], f["x_hat"]):
+        # diagnostics for a mismatch: its extent, and which side reproduces itself on a second call
+        dd = (d["x_hat"] - f["x_hat"]).abs()
+        f2 = net(xd, stage=2, s=levels)
+        d2 = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
+        net.set_precision(0)
+        f0 = net(xd, stage=2, s=levels)
+        net.set_precision(2)
+        info = {"n_diff": int((dd > 0).sum()), "max": float(dd.max()),
+                "per_image": [int((dd[i] > 0).sum()) for i in range(dd.shape[0])],
+                "forward_repeat_equal": torch.equal(f2["x_hat"], f["x_hat"]),
+                "decompress_repeat_equal": torch.equal(d2["x_hat"], d["x_hat"]),
+                "forward_is_fp32": torch.equal(f0["x_hat"], f["x_hat"]),
+                "decompress_is_fp32": torch.equal(f0["x_hat"], d["x_hat"])}
+        PARITY["vbr_4k_roundtrip_mismatch"] = info
+        raise AssertionError(info)
     for i, lv in enumerate(levels):
         fi = net(x[i:i + 1], stage=2, s=lv)
         assert torch.equal(fi["x_hat"], f["x_hat"][i:i + 1])
@@ -527,9 +540,22 @@ def test_vbr_4k_mixed_levels_vs_oracle_and_per_image():
     f = net(xd, stage=2, s=levels)
     c = net.compress(xd, stage=2, s=levels)
     d = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
-    dd = (d["x_hat"] - f["x_hat"]).abs()
-    assert torch.equal(d["x_hat"], f["x_hat"]), (int((dd > 0).sum()), float(dd.max()),
-                                                  [int((dd[i] > 0).sum()) for i in range(dd.shape[0])])
+    if not torch.equal(d["x_hat"], f["x_hat"]):
+        # diagnostics for a mismatch: its extent, and which side reproduces itself on a second call
+        dd = (d["x_hat"] - f["x_hat"]).abs()
+        f2 = net(xd, stage=2, s=levels)
+        d2 = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
+        net.set_precision(0)
+        f0 = net(xd, stage=2, s=levels)
+        net.set_precision(2)
+        info = {"n_diff": int((dd > 0).sum()), "max": float(dd.max()),
+                "per_image": [int((dd[i] > 0).sum()) for i in range(dd.shape[0])],
+                "forward_repeat_equal": torch.equal(f2["x_hat"], f["x_hat"]),
+                "decompress_repeat_equal": torch.equal(d2["x_hat"], d["x_hat"]),
+                "forward_is_fp32": torch.equal(f0["x_hat"], f["x_hat"]),
+                "decompress_is_fp32": torch.equal(f0["x_hat"], d["x_hat"])}
+        PARITY["vbr_4k_roundtrip_mismatch"] = info
+        raise AssertionError(info)
     for i, lv in enumerate(levels):
         fi = net(xd[i:i + 1], stage=2, s=lv)
         assert torch.equal(fi["x_hat"], f["x_hat"][i:i + 1])
