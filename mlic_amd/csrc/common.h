@@ -147,7 +147,11 @@ __device__ __forceinline__ mlic_float2 gelu_erf2(mlic_float2 x) {
 // up in registers); gelu_erf serves the chain kernel, where it is interleaved with MFMAs, and the
 // pw_resident / dwpw epilogues, whose element loops are short
 __device__ __forceinline__ float gelu_epi(float x) {
+#ifdef MLIC_GELU_EPI_FAST  // A/B build only: the chain kernel's branch-free form in the conv epilogues
+  return gelu_erf(x);
+#else
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+#endif
 }
 
 // GDN / IGDN output: x * rsqrt(v) / x * sqrt(v) on the hardware v_rsq / v_sqrt (1 ulp; v >= beta > 0)
