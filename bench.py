@@ -105,7 +105,7 @@ def parse():
     ap.add_argument("--profile-lanes", type=int, default=0,
                     help="lanes of the profiled step (0 = same as --lanes, so its launches match the timed "
                          "steps' and rocprofv3's per-kernel averages; 1 = isolated per-kernel times)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
                     help="PMC-derived HBM bytes per launch of the dominant family (tools/pmc_traffic.py)")
     ap.add_argument("--group-concurrency", type=int, default=0,
                     help="(weights, shape) batches of a step run concurrently, each on its own model "
@@ -441,7 +441,9 @@ def main():
             **prof,
             "host_thread_ms_per_step": host,
             "host_threads": int(os.environ.get("MLIC_HOST_THREADS", "0")),
-            "wall_ms_per_step": wall_split,
+            # per-phase wall time per step; with concurrent groups the phases of different groups overlap,
+            # so the sums may exceed the step (reported under a name that says so)
+            ("wall_ms_per_step" if conc == 1 else "wall_ms_per_step_summed_over_concurrent_groups"): wall_split,
             "lanes": a.lanes,
             "group_concurrency": conc,
             "batches_per_step": [len(js) for _, js in groups],
@@ -542,45 +544,61 @@ def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev):
         peak_tf, _ = kernel_peak(name)
         return 1e3 * max(fm["flops"] / (peak_tf * 1e12), fm["bytes"] / (PEAK_HBM_GBS * 1e9))
 
-    # dominant = the family with the most device time in the timed configuration (pass 1)
-    dom = max(fam, key=lambda k: fam[k]["ms"])
-    bound, unit, achieved, peak, arith = bound_of(fam[dom], dom)
-    iso = fam1.get(dom)
+    # The headline roofline is the kernel's own: launch durations of the isolated pass (one lane running
+    # one lane's share of the first batch, each launch alone on the GPU -- reproducible with
+    # `rocprofv3 --kernel-trace --stats -- python bench.py --lanes 1 --batch <share>`).  The timed
+    # configuration's launches overlap across lanes, so their HIP-event durations include other lanes'
+    # kernels; they are kept as the secondary `concurrent` entry.
+    # dominant = the family with the most isolated device time
+    dom = max(fam1, key=lambda k: fam1[k]["ms"]) if fam1 else max(fam, key=lambda k: fam[k]["ms"])
+    iso = fam1.get(dom) or fam[dom]
+    bound, unit, achieved, peak, arith = bound_of(iso, dom)
     t_roof = sum(t_roof_ms(v, k) for k, v in fam.items())
-    traffic = None
+    traffic, traffic_src = None, None
     try:
         with open(a.traffic_json) as f:
             tj = json.load(f)
         if tj.get("config", "main") == a.config and family(tj.get("family", "")) == dom:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = tj.get("launches_of")
     except (OSError, ValueError):
         pass
-    d = fam[dom]
+    # the isolated pass covers `share` images of the first batch; scaled to the step's pixels, the
+    # family's own time per step cannot exceed the measured step (it is one family of many)
+    step_px = sum(len(js) * H * W for (_, _, H, W), js in groups)
+    share_px = share * groups[0][0][2] * groups[0][0][3]
+    dom_ms_step = iso["ms"] * step_px / share_px
+    assert dom_ms_step <= 1e3 * t_step_s, (dom, dom_ms_step, 1e3 * t_step_s)
     roofline = {"bound": bound, "kernel": f"{dom} ({arith})",
                 "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / max(1, d["launches"]), 2),
-                "algorithmic_flops_per_launch": round(d["flops"] / max(1, d["launches"])),
-                "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"])),
-                "share_of_gpu_time": round(d["ms"] / max(1e-9, sum(v["ms"] for v in fam.values())), 4),
+                "traffic_launches": traffic_src,
+                "timing": f"isolated: HIP events around each launch, one lane, {share} image(s) of the first "
+                          f"batch, each launch alone on the GPU",
+                "launches_isolated": iso["launches"], "avg_launch_us": round(1000 * iso["ms"] / max(1, iso["launches"]), 2),
+                "algorithmic_flops_per_launch": round(iso["flops"] / max(1, iso["launches"])),
+                "algorithmic_bytes_per_launch": round(iso["bytes"] / max(1, iso["launches"])),
+                "family_ms_per_step_from_isolated": round(dom_ms_step, 3),
+                "share_of_isolated_gpu_time": round(iso["ms"] / max(1e-9, sum(v["ms"] for v in fam1.values())), 4),
                 # T_roof = sum_k max(F_k / P_k, B_k / BW) over every kernel of one step,
                 # against the measured step time
                 "step_t_roof_ms": round(t_roof, 3), "step_ms": round(1e3 * t_step_s, 3),
                 "step_frac": round(t_roof / max(1e-9, 1e3 * t_step_s), 4)}
-    # the runner-up families too (the top two are often within a few % of each other: the choice
-    # between them is not stable across boxes, and rocprofv3 may rank them the other way)
+    if dom in fam:
+        _, _, ach_c, _, _ = bound_of(fam[dom], dom)
+        roofline["concurrent"] = {"achieved": round(ach_c, 3), "frac": round(ach_c / peak, 4),
+                                  "lanes": prof_lanes, "launches_per_step": fam[dom]["launches"],
+                                  "avg_launch_us": round(1000 * fam[dom]["ms"] / max(1, fam[dom]["launches"]), 2),
+                                  "note": "launches of the timed configuration, overlapped across lanes"}
+    # the runner-up families (isolated), each with its own roofline fraction
     others = []
-    for k in sorted(fam, key=lambda k: -fam[k]["ms"])[1:3]:
-        b_, u_, a_, p_, _ = bound_of(fam[k], k)
+    for k in sorted(fam1, key=lambda k: -fam1[k]["ms"])[1:4]:
+        b_, u_, a_, p_, _ = bound_of(fam1[k], k)
         others.append({"kernel": k, "bound": b_, "achieved": round(a_, 3), "peak": round(p_, 1), "unit": u_,
-                       "frac": round(a_ / p_, 4), "launches_per_step": fam[k]["launches"],
-                       "avg_launch_us": round(1000 * fam[k]["ms"] / max(1, fam[k]["launches"]), 2),
-                       "share_of_gpu_time": round(fam[k]["ms"] / max(1e-9, sum(v["ms"] for v in fam.values())), 4)})
+                       "frac": round(a_ / p_, 4), "launches_isolated": fam1[k]["launches"],
+                       "avg_launch_us": round(1000 * fam1[k]["ms"] / max(1, fam1[k]["launches"]), 2),
+                       "share_of_isolated_gpu_time": round(fam1[k]["ms"] / max(1e-9, sum(v["ms"] for v in fam1.values())), 4)})
     roofline["runners_up"] = others
-    if iso:
-        _, _, ach1, _, _ = bound_of(iso, dom)
-        roofline["isolated"] = {"achieved": round(ach1, 3), "frac": round(ach1 / peak, 4), "images": share,
-                                "avg_launch_us": round(1000 * iso["ms"] / max(1, iso["launches"]), 2)}
     prof = {
         # with profile_lanes > 1 these are per-launch durations summed over concurrently running lanes
         "kernel_families_ms_per_step": {k: round(v["ms"], 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])},

@@ -65,6 +65,14 @@ int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32
 /* sum of -log2 of image b's y / z likelihoods in the last compress(): bpp_lik = (y + z) / (H * W) of the
  * unpadded image (loss/rd_loss.py:42-45) */
 int mlic_encoded_bits(mlic_model* m, int b, double* y_bits, double* z_bits);
+/* the reference's batched layout (models/mlicpp.py:215, 279-281: one y stream for a B > 1 batch,
+ * phase-major and image-minor; strings = [[y], [z_0 .. z_B-1]]): images [first, first + count) of the
+ * last compress coded into one stream (out = NULL queries the length; the coding runs on every call) */
+int mlic_batch_stream(mlic_model* m, int first, int count, uint8_t* out, size_t cap, size_t* len);
+/* decode such a stream (mlicpp.py:306-307 decodes strings[0][0] for the whole batch): one lane, the
+ * images of each phase in order */
+int mlic_decompress_batch_stream(mlic_model* m, void* stream, const uint8_t* y, size_t y_len, const uint8_t* const* z,
+                                 const size_t* z_len, int B, int hz, int wz, float* x_hat, const float* vbr_scales);
 /* y[b], z[b]: host byte strings of image b; hz, wz = latent z grid (shape returned by compress) */
 int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
                     const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
@@ -86,6 +94,15 @@ int mlic_set_precision(mlic_model* m, int precision);
  * x_hat only (forward / decompress); bitstreams and likelihoods are unaffected.  Gate: |dPSNR| <= 0.01 dB.
  * Also $MLIC_SYNTH_FP16=1. */
 int mlic_set_synthesis_precision(mlic_model* m, int mode);
+/* test switch: fill every workspace block with NaN (0xFF bytes) when it is handed out, so a kernel
+ * reading memory its producer never wrote fails visibly (also $MLIC_POISON=1).  Off by default. */
+int mlic_set_poison(mlic_model* m, int on);
+/* fp16 range-guard fallbacks taken since the last reset (each changes the arithmetic of one call):
+ * forward re-run whole in exact fp32 (the entropy model left fp16's range; compress refuses such an
+ * input), forward's g_s alone, decompress's g_s alone (the same policy on both sides, so
+ * decompress(compress(x)) == forward(x) bit for bit whenever compress succeeds) */
+int mlic_range_fallbacks(mlic_model* m, int64_t* forward_full, int64_t* forward_gs, int64_t* decompress_gs,
+                         int reset);
 /* live kernel timing (HIP events on the executor stream), one category per kernel family / tile
  * instantiation: mlic_profile_categories gives the count, mlic_profile_category_name the kernel
  * name of each.  read() sums and clears. */

@@ -45,6 +45,10 @@ def _sig(lib):
         "mlic_set_lanes": [p, i],
         "mlic_set_precision": [p, i],
         "mlic_set_synthesis_precision": [p, i],
+        "mlic_set_poison": [p, i],
+        "mlic_batch_stream": [p, i, i, p, sz, P(sz)],
+        "mlic_decompress_batch_stream": [p, p, p, sz, P(p), P(sz), i, i, i, p, p],
+        "mlic_range_fallbacks": [p, P(i64), P(i64), P(i64), i],
         "mlic_profile_layers": [p, p, sz, P(sz)],
         "mlic_bench_conv": [i, i, i, i, i, i, i, i, i, i, P(C.c_double), P(C.c_double)],
         "mlic_profile_read": [p, i, P(i64), P(C.c_double), P(C.c_double), P(C.c_double)],
@@ -83,6 +87,13 @@ def lib():
                                 f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
             _lib = _sig(C.CDLL(LIB_PATH))
     return _lib
+
+
+def poison() -> bool:
+    """$MLIC_POISON=1 (test switch): the executor NaN-fills its workspace blocks on allocation and the
+    Python layer NaN-fills the output tensors it hands to the library, so any element a kernel does
+    not write, or any read of memory its producer never wrote, shows up as NaN."""
+    return os.environ.get("MLIC_POISON", "0") not in ("", "0")
 
 
 def check(rc: int, what: str = ""):

@@ -64,6 +64,7 @@ int mlic_create(const char* model_name, int n, const char* const* names, const f
       if (const char* e = std::getenv("MLIC_LANES")) m->impl->set_lanes(std::atoi(e));
       if (const char* e = std::getenv("MLIC_PRECISION")) m->impl->set_precision(std::atoi(e));
       if (const char* e = std::getenv("MLIC_SYNTH_FP16")) m->impl->set_synthesis_precision(std::atoi(e) == 1 ? 1 : 0);
+      if (const char* e = std::getenv("MLIC_POISON")) m->impl->set_poison(std::atoi(e) != 0);
     } catch (...) {
       delete m;
       throw;
@@ -168,6 +169,28 @@ int mlic_decompress_v(mlic_model* m, void* stream, const uint8_t* const* y, cons
   });
 }
 
+int mlic_batch_stream(mlic_model* m, int first, int count, uint8_t* out, size_t cap, size_t* len) {
+  return guard([&] {
+    MLIC_CHECK(m && len, "bad arguments");
+    const std::string s = impl(m).batch_stream(first, count);
+    *len = s.size();
+    if (out) {
+      MLIC_CHECK(cap >= s.size(), "batch_stream: buffer too small");
+      std::memcpy(out, s.data(), s.size());
+    }
+  });
+}
+
+int mlic_decompress_batch_stream(mlic_model* m, void* stream, const uint8_t* y, size_t y_len, const uint8_t* const* z,
+                                 const size_t* z_len, int B, int hz, int wz, float* x_hat, const float* vbr_scales) {
+  return guard([&] {
+    MLIC_CHECK(m && y && z && x_hat && B > 0 && hz > 0 && wz > 0, "bad arguments");
+    const uint8_t* ys[1] = {y};
+    const size_t yl[1] = {y_len};
+    impl(m).decompress(ys, yl, z, z_len, B, hz, wz, x_hat, vbr_scales, (hipStream_t)stream, true);
+  });
+}
+
 int mlic_decompress(mlic_model* m, void* stream, const uint8_t* const* y, const size_t* y_len,
                     const uint8_t* const* z, const size_t* z_len, int B, int hz, int wz, float* x_hat,
                     float vbr_scale) {
@@ -191,6 +214,25 @@ int mlic_set_precision(mlic_model* m, int precision) {
   return guard([&] {
     MLIC_CHECK(precision >= PREC_F32 && precision <= PREC_F16X3_V2, "precision must be 0 (f32), 1 or 2 (f16x3)");
     impl(m).set_precision(precision);
+  });
+}
+
+int mlic_set_poison(mlic_model* m, int on) {
+  return guard([&] { impl(m).set_poison(on != 0); });
+}
+
+int mlic_range_fallbacks(mlic_model* m, int64_t* forward_full, int64_t* forward_gs, int64_t* decompress_gs,
+                         int reset) {
+  return guard([&] {
+    Model::Fallbacks& f = impl(m).fallbacks();
+    if (forward_full) *forward_full = f.forward_full.load();
+    if (forward_gs) *forward_gs = f.forward_gs.load();
+    if (decompress_gs) *decompress_gs = f.decompress_gs.load();
+    if (reset) {
+      f.forward_full = 0;
+      f.forward_gs = 0;
+      f.decompress_gs = 0;
+    }
   });
 }
 

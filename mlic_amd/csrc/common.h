@@ -90,10 +90,14 @@ struct ConvParams {
 };
 
 // device helpers -----------------------------------------------------------------------------
-// fp16 range guard at every activation split site: a value that does not fit fp16 (|v| >= 65520
-// rounds to inf; NaN included) is noted in a per-thread bit, and range_report raises *flag once per
-// thread at the end of the kernel; the executor then re-runs forward on the exact fp32 MFMA path, or
-// fails compress/decompress loudly (Model::range_hit / range_fail)
+// fp16 range guard: a split-fp16 operand that does not fit fp16 (|v| >= 65520 rounds to inf; NaN
+// included) raises the calling lane's device flag (Lane::rflag, range_report).  The conv kernels test
+// their split inputs; the chain kernel tests that its outputs are finite (an overflowing split operand
+// becomes +-inf, which its GELU turns into NaN and every later layer carries).  Model::range_hit reads
+// and clears the flag: an overflow in the entropy model makes forward() re-run whole in exact fp32 and
+// compress() / decompress() refuse the input (the decoder must reproduce the encoder's arithmetic); one
+// in g_s alone makes forward() and decompress() re-run g_s alone in exact fp32 (Model::gs_fp32_rerun).
+// Every fallback is counted (mlic_range_fallbacks).
 // softmax exponent on the hardware exp2 (one v_exp_f32 + one multiply instead of expf's ~12-instruction
 // range-reduced sequence): e^x = 2^(x log2 e).  Arguments are x - max <= 0; relative error
 // <= 1 ulp + |x| 2^-24 ln 2 (1e-7 at |x| = 1, 1e-6 at |x| = 20, where e^x < 3e-9 of the largest term).

@@ -26,7 +26,7 @@ Cfg config_for(const std::string& name) {  // config/config.py:19-62 (+ MLICPP_L
   else if (name == "MLICPP_S" || name == "MLICPP_S_VBR") { c.N = 96; c.M = 160; c.S = 5; }
   else if (name == "MLICPP_M") { c.N = 160; c.M = 256; c.S = 8; }
   else if (name == "MLICPP_S2") { c.N = 128; c.M = 128; c.S = 2; }
-  else if (name == "MLICPP_M_SMALL_DEC") { c.N = 192; c.M = 320; c.S = 10; c.sd = true; }
+  else if (name == "MLICPP_M_SMALL_DEC" || name == "MLICPP_M_SMALL_DEC_VBR") { c.N = 192; c.M = 320; c.S = 10; c.sd = true; }
   else throw Error("mlic: unknown model name " + name);
   c.vbr = name.size() > 4 && name.substr(name.size() - 4) == "_VBR";
   c.C = c.M / c.S;
@@ -53,6 +53,7 @@ float* Arena::alloc(int64_t nfloats) {
   peak_ = std::max(peak_, top_);
   if (dry_) return reinterpret_cast<float*>((uintptr_t)0x1000 + off);  // never dereferenced
   MLIC_CHECK(top_ <= cap_, "arena overflow (plan mismatch)");
+  if (poison_) HIP_OK(hipMemsetAsync(base_ + off, 0xFF, bytes, poison_st_));
   return reinterpret_cast<float*>(base_ + off);
 }
 
@@ -1111,24 +1112,31 @@ void Model::lrp(const std::vector<View>& ins, const std::string& kind, int i, co
 // ------------------------------------------------------------------------------------- phases
 class PhaseDecoder {
  public:
+  // single: y[0] holds every image's symbols, phase-major then image-minor (the reference's batched
+  // stream); one decoder then walks the images of each phase in order
   PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym, int32_t* h_idx,
-               HostStats* hs, HostPool* pool)
-      : t_(t), h_sym_(h_sym), h_idx_(h_idx), hs_(hs), pool_(pool) {
-    dec_.resize(B);
-    for (int b = 0; b < B; ++b) dec_[b].set_stream(y[b], ylen[b]);
+               HostStats* hs, HostPool* pool, bool single = false)
+      : t_(t), h_sym_(h_sym), h_idx_(h_idx), hs_(hs), pool_(pool), B_(B) {
+    dec_.resize(single ? 1 : B);
+    for (size_t b = 0; b < dec_.size(); ++b) dec_[b].set_stream(y[b], ylen[b]);
   }
   void run(int64_t n_per, hipStream_t st, int32_t* d_idx, int32_t* d_sym) {
-    const int B = (int)dec_.size();
+    const int B = B_;
     HIP_OK(hipMemcpyAsync(h_idx_, d_idx, sizeof(int32_t) * n_per * B, hipMemcpyDeviceToHost, st));
     {
       HostStats::Scope w{hs_->wait_ns};
       HIP_OK(hipStreamSynchronize(st));
     }
-    auto work = [&](int b) {
+    if ((int)dec_.size() == 1 && B > 1) {
       HostStats::Scope d{hs_->dec_ns};
-      dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per);
-    };
-    pool_->run(B, work);
+      dec_[0].decode(h_idx_, n_per * B, *t_, h_sym_);  // [B][n_per] of this phase = the stream's order
+    } else {
+      auto work = [&](int b) {
+        HostStats::Scope d{hs_->dec_ns};
+        dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per);
+      };
+      pool_->run(B, work);
+    }
     HIP_OK(hipMemcpyAsync(d_sym, h_sym_, sizeof(int32_t) * n_per * B, hipMemcpyHostToDevice, st));
   }
 
@@ -1139,6 +1147,7 @@ class PhaseDecoder {
   int32_t* h_idx_;
   HostStats* hs_;
   HostPool* pool_;
+  int B_;
 };
 
 // mlicpp.py:107-176 (forward), 220-277 (compress), 309-366 (decompress)
@@ -1266,6 +1275,11 @@ void Model::planned(int B, hipStream_t st, F&& body) {
   l.dry = false;
   l.arena.ensure(need + (1 << 20));
   l.arena.begin(false);
+  if (poison_) l.arena.poison_on(l.st);
+  struct Off {
+    Arena& a;
+    ~Off() { a.poison_off(); }
+  } off{l.arena};
   body();
 }
 
@@ -1387,8 +1401,8 @@ ProfStat Model::profile_read(int cat) {
 }
 
 template <class F>
-void Model::over_lanes(int B, hipStream_t caller, F&& fn) {
-  const int nl = std::max(1, std::min(nlanes_, B));
+void Model::over_lanes(int B, hipStream_t caller, F&& fn, int max_lanes) {
+  const int nl = std::max(1, std::min(std::min(nlanes_, max_lanes), B));
   hipEvent_t ready;
   HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
   HIP_OK(hipEventRecord(ready, caller));  // inputs produced on the caller's stream
@@ -1439,6 +1453,15 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
   l.st = st;  // caller's stream, including the legacy NULL stream torch uses by default
   set_vbr(vbr_scales, B);
   range_clear(l);
+  // The fp16 range guard needs a device-to-host read, i.e. a synchronisation of `st`; under stream
+  // capture (hipGraph) there is none, and a captured forward cannot fall back: its flag stays set
+  // for the caller to read.  Otherwise forward() returns with `st` synchronised.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_OK(hipStreamIsCapturing(st, &cap));
+  const bool guard = cap == hipStreamCaptureStatusNone && prec() != PREC_F32;
+  bool entropy_hit = false;
+  View yhat;
+  const View out{x_hat, 3, H, W, (int64_t)3 * H * W};
   auto body = [&] {
     View xv{const_cast<float*>(x), 3, H, W, (int64_t)3 * H * W};
     View y = g_a(xv);
@@ -1446,26 +1469,44 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
     View zh = alloc(z.C, z.H, z.W);
     eb(z, zh, z_lik, nullptr);
     View hyper = h_s(zh);
-    View yhat = alloc(cfg_.M, y.H, y.W);
+    yhat = alloc(cfg_.M, y.H, y.W);
     slice_loop(Mode::Forward, hyper, &y, yhat, y_lik, nullptr, nullptr, nullptr);
-    if (x_hat) {
-      View out{x_hat, 3, H, W, (int64_t)3 * H * W};
-      g_s(yhat, out);
-    }
+    // the same policy as compress / decompress: an overflow in the entropy model (g_a .. slice loop)
+    // re-runs the whole call in exact fp32 (compress refuses such an input); one in g_s alone re-runs
+    // g_s alone, as decompress does, so decompress(compress(x)) == forward(x) bit for bit
+    if (guard && !l.dry && prec() != PREC_F32) entropy_hit = range_hit(l);
+    if (x_hat && !entropy_hit) g_s(yhat, out);
   };
   planned(B, st, body);
-  // The fp16 range guard needs a device-to-host read, i.e. a synchronisation of `st`; under stream
-  // capture (hipGraph) there is none, and a captured forward cannot fall back: its flag stays set
-  // for the caller to read.  Otherwise forward() returns with `st` synchronised.
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  HIP_OK(hipStreamIsCapturing(st, &cap));
-  if (cap == hipStreamCaptureStatusNone && prec() != PREC_F32 && range_hit(l)) {
-    // an activation left fp16's range in a split-fp16 kernel: the whole call again in exact fp32 MFMA
+  if (entropy_hit) {
+    fb_.forward_full++;
+    entropy_hit = false;
     l.prec_force = PREC_F32;
     planned(B, st, body);
     l.prec_force = -1;
     (void)range_hit(l);
+    return;
   }
+  if (guard && range_hit(l) && x_hat) {
+    fb_.forward_gs++;
+    gs_fp32_rerun(l, yhat, out, B);
+  }
+}
+
+void Model::gs_fp32_rerun(Lane& l, const View& yhat, const View& out, int B) {
+  const size_t nb = sizeof(float) * (size_t)B * yhat.bs;
+  float* keep = nullptr;
+  HIP_OK(hipMalloc(&keep, nb));
+  struct Free {
+    float* p;
+    Lane& l;
+    ~Free() { l.prec_force = -1; (void)hipStreamSynchronize(l.st); (void)hipFree(p); }
+  } fr{keep, l};
+  HIP_OK(hipMemcpyAsync(keep, yhat.p, nb, hipMemcpyDeviceToDevice, l.st));
+  l.prec_force = PREC_F32;
+  planned(B, l.st, [&] { g_s(View{keep, yhat.C, yhat.H, yhat.W, yhat.bs}, out); });
+  l.prec_force = -1;
+  (void)range_hit(l);
 }
 
 // the fp16 range guard (common.h range_check): read and clear the lane's device flag
@@ -1585,19 +1626,37 @@ HostPool& Model::host_pool() {
 }
 
 void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
-                       int B, int hz, int wz, float* x_hat, const float* vbr_scales, hipStream_t st) {
+                       int B, int hz, int wz, float* x_hat, const float* vbr_scales, hipStream_t st, bool batch_stream) {
   MLIC_CHECK(!gc_.empty() && !eb_.empty(), "entropy tables not set: call update() first");
   const int64_t img = (int64_t)3 * 64 * hz * 64 * wz;
   over_lanes(B, st, [&](Lane& l, int first, int cnt) {
     set_vbr(vbr_scales ? vbr_scales + first : nullptr, cnt);
-    decompress_lane(y + first, ylen + first, z + first, zlen + first, cnt, hz, wz, x_hat + first * img);
-  });
+    decompress_lane(batch_stream ? y : y + first, batch_stream ? ylen : ylen + first, z + first, zlen + first, cnt, hz,
+                    wz, x_hat + first * img, batch_stream);
+  }, batch_stream ? 1 : 16);
+}
+
+std::string Model::batch_stream(int first, int count) const {
+  MLIC_CHECK(first >= 0 && count >= 1 && first + count <= (int)enc_all_.size(), "batch_stream: image range");
+  const size_t n = enc_all_[first].y_sym.size();
+  const int64_t n_per = (int64_t)n / (2 * cfg_.S);
+  std::vector<int32_t> s, ix;
+  s.reserve(n * count);
+  ix.reserve(n * count);
+  for (int k = 0; k < 2 * cfg_.S; ++k)
+    for (int b = first; b < first + count; ++b) {
+      const EncodedImage& e = enc_all_[b];
+      MLIC_CHECK(e.y_sym.size() == n, "batch_stream: images of one shape");
+      s.insert(s.end(), e.y_sym.begin() + k * n_per, e.y_sym.begin() + (k + 1) * n_per);
+      ix.insert(ix.end(), e.y_idx.begin() + k * n_per, e.y_idx.begin() + (k + 1) * n_per);
+    }
+  return rans_encode(s.data(), ix.data(), (int64_t)s.size(), gc_);
 }
 
 // mlicpp.py:292-378 for the lane's images: z decoded on the host, then 20 phases of
 // (network -> indexes D2H -> per-image host rANS decode -> symbols H2D -> dequantise)
 void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z,
-                            const size_t* zlen, int B, int hz, int wz, float* x_hat) {
+                            const size_t* zlen, int B, int hz, int wz, float* x_hat, bool batch_stream) {
   Lane& l = L();
   const int h = hz * 4, w = wz * 4;
   const int64_t n_per = (int64_t)cfg_.C * h * (w / 2);
@@ -1612,7 +1671,7 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
       d.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
     }
   }
-  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool());
+  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool(), batch_stream);
   const int32_t* hz_sym = l.h_sym;
   range_clear(l);
   View yhat;
@@ -1636,18 +1695,9 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
   });
   if (prec() != PREC_F32 && range_hit(l)) {
     // only the synthesis transform left fp16's range: y_hat is final, so re-run g_s alone in exact
-    // fp32 MFMA (as forward() re-runs), from a copy of y_hat (the re-plan may move the arena)
-    const size_t nb = sizeof(float) * (size_t)B * yhat.bs;
-    float* keep = nullptr;
-    HIP_OK(hipMalloc(&keep, nb));
-    struct Free {
-      float* p;
-      Lane& l;
-      ~Free() { l.prec_force = -1; (void)hipStreamSynchronize(l.st); (void)hipFree(p); }
-    } fr{keep, l};
-    HIP_OK(hipMemcpyAsync(keep, yhat.p, nb, hipMemcpyDeviceToDevice, l.st));
-    l.prec_force = PREC_F32;
-    planned(B, nullptr, [&] { g_s(View{keep, cfg_.M, h, w, yhat.bs}, out); });
+    // fp32 MFMA (forward() takes the same fallback)
+    fb_.decompress_gs++;
+    gs_fp32_rerun(l, yhat, out, B);
   }
 }
 

@@ -66,11 +66,18 @@ class Arena {
   void begin(bool dry) { dry_ = dry; top_ = 0; peak_ = 0; }
   size_t peak() const { return peak_; }
   size_t capacity() const { return cap_; }
+  // test switch ($MLIC_POISON / mlic_set_poison): every block handed out by alloc() is filled with
+  // 0xFF bytes (a NaN in every fp32 / fp16 lane) on `st` first, so a kernel that reads arena memory
+  // its producer never wrote poisons its output instead of silently reading a previous call's data
+  void poison_on(hipStream_t st) { poison_st_ = st; poison_ = true; }
+  void poison_off() { poison_ = false; }
 
  private:
   char* base_ = nullptr;
   size_t cap_ = 0, top_ = 0, peak_ = 0;
   bool dry_ = false;
+  bool poison_ = false;
+  hipStream_t poison_st_ = nullptr;
 };
 
 // live per-kernel-family timing with HIP events on the executor's stream (bench.py roofline);
@@ -149,8 +156,14 @@ class Model {
   void compress(const float* x, int B, int H, int W, const float* vbr_scales, hipStream_t st);
   const EncodedImage& encoded(int b) const { return enc_all_.at(b); }
   // decompress(): y/z byte streams per image -> x_hat [B,3,4*16*hz,4*16*wz]
+  // batch_stream: y[0] is ONE stream holding the whole batch in the reference's order (mlicpp.py:215,
+  // 279-281: phase-major, image-minor); decoded on one lane (the stream is sequential)
   void decompress(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen, int B,
-                  int hz, int wz, float* x_hat, const float* vbr_scales, hipStream_t st);
+                  int hz, int wz, float* x_hat, const float* vbr_scales, hipStream_t st, bool batch_stream = false);
+  // the last compress()'s images [first, first + count) coded into ONE y stream in the reference's
+  // batched order (mlicpp.py:215, 279-281): byte-identical to what the reference's compress() emits for
+  // that batch when it codes the same symbols
+  std::string batch_stream(int first, int count) const;
   void set_tables(const CdfTables& gc, const CdfTables& eb) {
     gc_ = gc;
     eb_ = eb;
@@ -165,6 +178,15 @@ class Model {
   void set_synthesis_precision(int p) { gs_fp16_ = p == 1; }
   int synthesis_precision() const { return gs_fp16_ ? 1 : 0; }
   int lanes() const { return nlanes_; }
+  // test switch: NaN-fill every arena block on allocation (Arena::poison_on); also $MLIC_POISON=1
+  void set_poison(bool on) { poison_ = on; }
+  // fp16 range-guard fallbacks taken since the last reset (they change the arithmetic of a call, so the
+  // round-trip tests assert they are 0): forward re-run whole in exact fp32 (the entropy model left
+  // fp16's range), forward's g_s alone, decompress's g_s alone
+  struct Fallbacks {
+    std::atomic<int64_t> forward_full{0}, forward_gs{0}, decompress_gs{0};
+  };
+  Fallbacks& fallbacks() { return fb_; }
   ProfStat profile_read(int cat);  // synchronises the recorded events; clears that category
   std::string profile_layers();     // per-tag table of the recorded events (does not clear)
   size_t weight_bytes() const { return wbytes_; }
@@ -209,6 +231,10 @@ class Model {
   bool gs_fp16_ = false;
   HostStats hstats_;
   bool prof_ = false;
+  bool poison_ = false;
+  Fallbacks fb_;
+  // re-run g_s alone in exact fp32 MFMA from a copy of y_hat (the re-plan may move the arena)
+  void gs_fp32_rerun(Lane& l, const View& yhat, const View& out, int B);
   static thread_local Lane* tl_lane_;
   Lane& L() const { return *tl_lane_; }
   Lane& lane(int i);
@@ -217,10 +243,10 @@ class Model {
   void timed(int cat, double flops, double bytes, F&& launch, const std::string& tag = std::string());
   // run fn(lane, first_image, count) over the batch split across lanes (host threads)
   template <class F>
-  void over_lanes(int B, hipStream_t caller, F&& fn);
+  void over_lanes(int B, hipStream_t caller, F&& fn, int max_lanes = 16);
   void compress_lane(const float* x, int B, int H, int W);
   void decompress_lane(const uint8_t* const* y, const size_t* ylen, const uint8_t* const* z, const size_t* zlen,
-                       int B, int hz, int wz, float* x_hat);
+                       int B, int hz, int wz, float* x_hat, bool batch_stream);
 
   // -- weights
   const ConvW& cw(const std::string& k) const;

@@ -177,6 +177,23 @@ class MLICPlusPlus(nn.Module):
             _lib.call("mlic_set_lanes", self._handle, self._lanes)
 
     @staticmethod
+    def _out(shape, dev):
+        """An output buffer: uninitialised, or NaN under the $MLIC_POISON test switch (an element the
+        library does not write then fails every equality and finiteness check)."""
+        if _lib.poison():
+            return torch.full(tuple(shape), float("nan"), device=dev)
+        return torch.empty(tuple(shape), device=dev)
+
+    def range_fallbacks(self, reset: bool = False) -> Dict[str, int]:
+        """fp16 range-guard fallbacks taken by this model since the last reset (mlic_range_fallbacks):
+        forward re-run whole in exact fp32, forward's g_s alone, decompress's g_s alone."""
+        if self._handle is None:
+            return {"forward_full": 0, "forward_gs": 0, "decompress_gs": 0}
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        _lib.call("mlic_range_fallbacks", self._handle, C.byref(a), C.byref(b), C.byref(c), int(reset))
+        return {"forward_full": a.value, "forward_gs": b.value, "decompress_gs": c.value}
+
+    @staticmethod
     def _stream():
         return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -196,9 +213,9 @@ class MLICPlusPlus(nn.Module):
             raise ValueError("H and W must be multiples of 64 (pad as utils/testing.py:130-137)")
         h = self._ensure_handle(x.device)
         x = x.contiguous().float()
-        x_hat = torch.empty_like(x)
-        y_lik = torch.empty(B, self.M, H // 16, W // 16, device=x.device)
-        z_lik = torch.empty(B, self.N, H // 64, W // 64, device=x.device)
+        x_hat = self._out(x.shape, x.device)
+        y_lik = self._out((B, self.M, H // 16, W // 16), x.device)
+        z_lik = self._out((B, self.N, H // 64, W // 64), x.device)
         sc = self._vbr_scales(B, **kw)
         _lib.call("mlic_forward_v", h, self._stream(), x.data_ptr(), B, H, W, x_hat.data_ptr(), y_lik.data_ptr(),
                   z_lik.data_ptr(), sc.ctypes.data)
@@ -250,9 +267,11 @@ class MLICPlusPlus(nn.Module):
         self._tables_pushed = h
 
     @torch.no_grad()
-    def compress(self, x: torch.Tensor, **kw):
+    def compress(self, x: torch.Tensor, batch_stream: bool = False, **kw):
         """mlicpp.py:199-290.  strings = [[y_stream per image], [z_stream per image]] (B = 1: exactly
-        the reference's layout; for B > 1 each image gets its own y stream instead of one shared one).
+        the reference's layout; for B > 1 each image gets its own y stream, which the host codes in
+        parallel).  batch_stream=True: the reference's B > 1 layout instead, ONE y stream for the batch
+        (mlicpp.py:215, 279-281; phase-major, image-minor).  decompress() accepts both.
         cost_time brackets the call with the caller's stream synchronised (the reference synchronises the
         whole device, mlicpp.py:200, 282; a stream keeps concurrent callers on other streams apart)."""
         torch.cuda.current_stream(x.device).synchronize()
@@ -274,6 +293,12 @@ class MLICPlusPlus(nn.Module):
             _lib.call("mlic_encoded_copy", h, b, yb, zb)
             ys.append(C.string_at(yb, yl.value))
             zs.append(C.string_at(zb, zl.value))
+        if batch_stream and B > 1:
+            n = C.c_size_t()
+            _lib.call("mlic_batch_stream", h, 0, B, None, 0, C.byref(n))
+            buf = C.create_string_buffer(max(1, n.value))
+            _lib.call("mlic_batch_stream", h, 0, B, buf, n.value, C.byref(n))
+            ys = [C.string_at(buf, n.value)]
         torch.cuda.current_stream(x.device).synchronize()
         return {"strings": [ys, zs], "shape": torch.Size([H // 64, W // 64]), "cost_time": time.time() - t0}
 
@@ -285,12 +310,13 @@ class MLICPlusPlus(nn.Module):
         t0 = time.time()
         ys, zs = list(strings[0]), list(strings[1])
         B = len(zs)
-        if len(ys) != B:
-            raise ValueError("expected one y stream per image")
+        single = len(ys) == 1 and B > 1  # the reference's batched layout (mlicpp.py:306-307)
+        if len(ys) != B and not single:
+            raise ValueError("expected one y stream per image, or one stream for the whole batch")
         hz, wz = int(shape[0]), int(shape[1])
         h = self._ensure_handle(dev)
         self._push_tables(h)
-        x_hat = torch.empty(B, 3, hz * 64, wz * 64, device=dev)
+        x_hat = self._out((B, 3, hz * 64, wz * 64), dev)
         ybufs = [C.create_string_buffer(s, len(s)) for s in ys]
         zbufs = [C.create_string_buffer(s, len(s)) for s in zs]
         yp = (C.c_void_p * B)(*[C.cast(b, C.c_void_p) for b in ybufs])
@@ -298,8 +324,12 @@ class MLICPlusPlus(nn.Module):
         yl = (C.c_size_t * B)(*[len(s) for s in ys])
         zl = (C.c_size_t * B)(*[len(s) for s in zs])
         sc = self._vbr_scales(B, **kw)
-        _lib.call("mlic_decompress_v", h, self._stream(), yp, yl, zp, zl, B, hz, wz, x_hat.data_ptr(),
-                  sc.ctypes.data)
+        if single:
+            _lib.call("mlic_decompress_batch_stream", h, self._stream(), C.cast(ybufs[0], C.c_void_p), len(ys[0]), zp,
+                      zl, B, hz, wz, x_hat.data_ptr(), sc.ctypes.data)
+        else:
+            _lib.call("mlic_decompress_v", h, self._stream(), yp, yl, zp, zl, B, hz, wz, x_hat.data_ptr(),
+                      sc.ctypes.data)
         torch.cuda.current_stream(dev).synchronize()
         return {"x_hat": x_hat, "cost_time": time.time() - t0}
 
@@ -332,7 +362,7 @@ class MLICPlusPlus(nn.Module):
         """Single-module execution through the C ABI (tests/profiling)."""
         h = self._ensure_handle(in0.device)
         B, Cin, H, W = in0.shape
-        out = torch.empty(out_shape, device=in0.device)
+        out = self._out(out_shape, in0.device)
         _lib.call("mlic_run_module", h, self._stream(), which.encode(), idx, in0.contiguous().data_ptr(),
                   None if in1 is None else in1.contiguous().data_ptr(), B, Cin, H, W, out.data_ptr())
         return out
@@ -352,7 +382,7 @@ class MLICPlusPlusVbr(MLICPlusPlus):
 
     def __init__(self, config=None, name: str = "MLICPP_L_VBR", **kw):
         super().__init__(config, name=name, **kw)
-        self.lmbda = list(spec.VBR_LAMBDAS)
+        self.lmbda = list(spec.vbr_lambdas(name))
         self.levels = len(self.lmbda)
 
     def _vbr_scales(self, B: int, stage: int = 2, s=1, inputscale=0, coder: bool = False, **kw) -> np.ndarray:
@@ -380,11 +410,20 @@ class MLICPlusPlusVbr(MLICPlusPlus):
     def forward(self, x, stage: int = 2, s=1, inputscale=0):
         return super().forward(x, stage=stage, s=s, inputscale=inputscale)
 
-    def compress(self, x, stage: int = 2, s=1, inputscale=0):
-        return super().compress(x, stage=stage, s=s, inputscale=inputscale, coder=True)
+    def compress(self, x, stage: int = 2, s=1, inputscale=0, batch_stream: bool = False):
+        return super().compress(x, batch_stream=batch_stream, stage=stage, s=s, inputscale=inputscale, coder=True)
 
     def decompress(self, strings, shape, stage: int = 2, s=1, inputscale=0):
         return super().decompress(strings, shape, stage=stage, s=s, inputscale=inputscale, coder=True)
+
+
+class MLICPlusPlusSDVbr(MLICPlusPlusVbr):
+    """MLICPP_M_SMALL_DEC_VBR (models/mlicpp_sd_vbr.py:19-1226): the small-decoder tree of
+    mlicpp_small_decoder.py with mlicpp_vbr.py's stage-2 Gain[s] scale/rescale (forward / compress /
+    decompress are line-for-line those of mlicpp_vbr.py), over five levels (Gain 0.002424 .. 1)."""
+
+    def __init__(self, config=None, name: str = "MLICPP_M_SMALL_DEC_VBR", **kw):
+        super().__init__(config, name=name, **kw)
 
 
 def model_config(model_name: str = "MLICPP_S"):
@@ -395,6 +434,8 @@ def model_config(model_name: str = "MLICPP_S"):
 def get_model(model_name: str) -> MLICPlusPlus:
     """models/model_loader.py:4-18 (+ MLICPP_L_VBR)."""
     cfg = spec.get_config(model_name)
+    if cfg.small_decoder and cfg.vbr:
+        return MLICPlusPlusSDVbr(name=model_name)
     if cfg.small_decoder:
         return MLICPlusPlusSD(name=model_name)
     if cfg.vbr:

@@ -10,6 +10,7 @@ every parameter and buffer, per model variant:
 * MLICPlusPlus ....... MLIC++/models/mlicpp.py:14-77
 * MLICPlusPlusSD ..... MLIC++/models/mlicpp_small_decoder.py:16-83
 * MLICPlusPlusVbr .... MLIC++/models/mlicpp_vbr.py:14-120
+* MLICPlusPlusSDVbr .. MLIC++/models/mlicpp_sd_vbr.py:19-118 (the small-decoder tree + the VBR gains)
 * layer naming ....... MLIC++/modules/layers/{conv,res_blk,attention}.py,
                        MLIC++/modules/transform/*.py, compressai 1.2.6 layers
 
@@ -61,11 +62,27 @@ CONFIGS: Dict[str, ModelConfig] = {
     "MLICPP_M": ModelConfig("MLICPP_M", 160, 256, 8),
     "MLICPP_S2": ModelConfig("MLICPP_S2", 128, 128, 2),
     "MLICPP_M_SMALL_DEC": ModelConfig("MLICPP_M_SMALL_DEC", 192, 320, 10, small_decoder=True),
+    # models/model_loader.py:14-15, config/config.py:52-59 (the MLICPP_M_SMALL_DEC dimensions)
+    "MLICPP_M_SMALL_DEC_VBR": ModelConfig("MLICPP_M_SMALL_DEC_VBR", 192, 320, 10, small_decoder=True, vbr=True),
 }
 
 # VBR constants, mlicpp_vbr.py:83-91
 VBR_LAMBDAS = (0.0005, 0.0035, 0.0067, 0.025, 0.0483, 0.18)
 VBR_GAIN = (0.06556, 0.13944, 0.19293, 0.37268, 0.51801, 1.00000)
+# the small-decoder VBR model's five levels, mlicpp_sd_vbr.py:89-97
+SD_VBR_LAMBDAS = (0.0002, 0.0005, 0.0035, 0.0483, 0.18)
+SD_VBR_GAIN = (0.002424, 0.06556, 0.13944, 0.51801, 1.00000)
+
+
+def vbr_lambdas(name: str) -> Tuple[float, ...]:
+    cfg = get_config(name)
+    return SD_VBR_LAMBDAS if cfg.small_decoder else VBR_LAMBDAS
+
+
+def vbr_gain(name: str) -> Tuple[float, ...]:
+    """The Gain parameter's initial value (= its trained size) of a VBR model."""
+    cfg = get_config(name)
+    return SD_VBR_GAIN if cfg.small_decoder else VBR_GAIN
 
 
 def get_config(name: str) -> ModelConfig:
@@ -275,7 +292,7 @@ def state_dict_shapes(name: str) -> "OrderedDict[str, Shape]":
             for j, (a, b) in enumerate(lrp_dims(cfg, cin)):
                 inv.dwsep(f"{p}.{2 * j}", a, b)
     if cfg.vbr:
-        inv.add("Gain", (len(VBR_GAIN),))
+        inv.add("Gain", (len(vbr_gain(name)),))
         inv.linear("QuantABCD.0", 2, 12)
         inv.linear("QuantABCD.2", 12, 12)
         inv.linear("QuantABCD.4", 12, 1)

@@ -105,7 +105,7 @@ def _draw(key: str, shape, cfg: spec.ModelConfig, seed: int) -> np.ndarray:
     if leaf == "relative_position_table":
         return (0.3 * r.standard_normal(n)).reshape(shape).astype(np.float32)
     if leaf == "Gain":
-        return np.array(spec.VBR_GAIN, np.float32)
+        return np.array(spec.vbr_gain(cfg.name), np.float32)
     # ---- conv / linear weights and biases -----------------------------------
     if leaf == "bias":
         return (0.05 * r.standard_normal(n)).reshape(shape).astype(np.float32)

@@ -228,9 +228,32 @@ def gen_forward(name, H, W, seed=0, img_seed=0, s=None, with_streams=False, rate
     print(f"  {tag}: bpp={bpp:.4f}")
 
 
+def gen_batch_streams(name="MLICPP_S", H=128, W=192, seeds=(40, 41, 42)):
+    """The reference's coder inputs for a B > 1 batch (mlicpp.py:215, 279-281): ONE symbol / index
+    list for the whole batch, in its own order (phase-major, image-minor), and the z symbols."""
+    m, sd = _ref_model(name, 0)
+    m.update(force=True)
+    x = torch.cat([synthetic.synth_image(H, W, s_) for s_ in seeds])
+    enc_mod = sys.modules[type(m).__module__]
+    captured = {}
+
+    class Enc:
+        def encode_with_indexes(self, symbols, indexes, cdf, lengths, offsets):
+            captured["sym"], captured["idx"] = symbols, indexes
+
+        def flush(self):
+            return b""
+    enc_mod.BufferedRansEncoder = Enc
+    with torch.no_grad():
+        c = m.compress(x)
+    save(f"batch_streams_{name}_{len(seeds)}x{H}x{W}.npz", y_symbols=np.asarray(captured["sym"], np.int32),
+         y_indexes=np.asarray(captured["idx"], np.int32), n_y_strings=len(c["strings"][0]),
+         n_z_strings=len(c["strings"][1]), seeds=np.asarray(seeds), sd_sha=sd_checksum(sd), x_sha=t_checksum(x))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    what = sys.argv[1:] or ["bitexact", "modules", "forward", "rates", "eb", "svbr"]
+    what = sys.argv[1:] or ["bitexact", "modules", "forward", "rates", "eb", "svbr", "sdvbr", "batch"]
     if "eb" in what:
         gen_eb()
     if "svbr" in what:
@@ -238,6 +261,13 @@ def main():
         for s in (0, 3, 5):
             gen_forward("MLICPP_S_VBR", 128, 128, s=s, with_streams=True)
         gen_forward("MLICPP_S_VBR", 192, 256, img_seed=3, s=1, with_streams=True)
+    if "batch" in what:
+        gen_batch_streams()
+    if "sdvbr" in what:
+        # MLICPP_M_SMALL_DEC_VBR (models/model_loader.py:14-15, models/mlicpp_sd_vbr.py)
+        for s in (0, 3):
+            gen_forward("MLICPP_M_SMALL_DEC_VBR", 128, 128, s=s, with_streams=True)
+        gen_forward("MLICPP_M_SMALL_DEC_VBR", 192, 256, img_seed=3, rate=1, s=2, with_streams=True)
     if "bitexact" in what:
         gen_bitexact()
     if "modules" in what:

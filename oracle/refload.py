@@ -40,7 +40,9 @@ def build(name):
     from mlic_amd import spec
     cfg = spec.get_config(name)
     c = _Cfg(N=cfg.N, M=cfg.M, slice_num=cfg.slice_num, context_window=cfg.context_window, act=nn.GELU)
-    if cfg.small_decoder:
+    if cfg.small_decoder and cfg.vbr:
+        cls = load_module("models/mlicpp_sd_vbr.py").MLICPlusPlusSDVbr
+    elif cfg.small_decoder:
         cls = load_module("models/mlicpp_small_decoder.py").MLICPlusPlusSD
     elif cfg.vbr:
         cls = load_module("models/mlicpp_vbr.py").MLICPlusPlusVbr

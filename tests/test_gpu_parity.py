@@ -42,6 +42,26 @@ def _dump_parity():
             json.dump(old, f, indent=1, sort_keys=True)
 
 
+# fp16 range-guard fallbacks (mlic_range_fallbacks) change a call's arithmetic: none may fire on any
+# cached net of this module (the range-guard tests build their own nets); counted into PARITY
+FALLBACKS = {"forward_full": 0, "forward_gs": 0, "decompress_gs": 0}
+
+
+@pytest.fixture(autouse=True)
+def _no_range_fallbacks(request):
+    yield
+    from mlic_amd import _lib
+    hit = {}
+    for key, n in list(_NETS.items()) + list(_RATE_NETS.items()):
+        fb = n.range_fallbacks(reset=True)
+        for k, v in fb.items():
+            FALLBACKS[k] += v
+        if any(fb.values()):
+            hit[str(key)] = fb
+    PARITY["range_fallbacks"] = dict(FALLBACKS, poison=_lib.poison())
+    assert not hit, (request.node.name, hit)
+
+
 def net_for(name, seed=0):
     key = (name, seed)
     if key not in _NETS:
@@ -111,7 +131,8 @@ def test_module_vectors(golden):
 FWD = [("MLICPP_L", 128, 192, None), ("MLICPP_L", 128, 128, None), ("MLICPP_S", 128, 128, None),
        ("MLICPP_S2", 128, 128, None), ("MLICPP_M", 128, 128, None), ("MLICPP_M_SMALL_DEC", 128, 128, None),
        ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5),
-       ("MLICPP_S_VBR", 128, 128, 0), ("MLICPP_S_VBR", 128, 128, 3), ("MLICPP_S_VBR", 128, 128, 5)]
+       ("MLICPP_S_VBR", 128, 128, 0), ("MLICPP_S_VBR", 128, 128, 3), ("MLICPP_S_VBR", 128, 128, 5),
+       ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 0), ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 3)]
 
 
 @pytest.mark.parametrize("name,H,W,s", FWD)
@@ -154,7 +175,8 @@ def test_forward_matches_oracle_batched(name, B, H, W):
 @pytest.mark.parametrize("name,H,W,s,img", [("MLICPP_L", 128, 192, None, 0), ("MLICPP_S", 128, 128, None, 0),
                                             ("MLICPP_M_SMALL_DEC", 128, 128, None, 0), ("MLICPP_S_VBR", 128, 128, 0, 0),
                                             ("MLICPP_S_VBR", 128, 128, 3, 0), ("MLICPP_S_VBR", 128, 128, 5, 0),
-                                            ("MLICPP_S_VBR", 192, 256, 1, 3)])
+                                            ("MLICPP_S_VBR", 192, 256, 1, 3), ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 0, 0),
+                                            ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 3, 0)])
 def test_compress_streams_match_reference(golden, name, H, W, s, img):
     """Coder inputs vs the exact symbol/index lists the reference hands to its rANS encoder (VBR: the
     values a consistent codec codes, taken from the reference forward, oracle/gen_golden.py).
@@ -186,7 +208,8 @@ def test_compress_streams_match_reference(golden, name, H, W, s, img):
 
 @pytest.mark.parametrize("name,B,H,W,s", [("MLICPP_L", 1, 128, 192, None), ("MLICPP_L", 2, 128, 128, None),
                                           ("MLICPP_S", 1, 192, 128, None), ("MLICPP_M_SMALL_DEC", 1, 128, 128, None),
-                                          ("MLICPP_L_VBR", 1, 128, 128, 2), ("MLICPP_S_VBR", 2, 128, 192, 4)])
+                                          ("MLICPP_L_VBR", 1, 128, 128, 2), ("MLICPP_S_VBR", 2, 128, 192, 4),
+                                          ("MLICPP_M_SMALL_DEC_VBR", 2, 128, 192, 3)])
 def test_roundtrip_bitexact(name, B, H, W, s):
     """decompress(compress(x)).x_hat == forward(x).x_hat, bit for bit (same kernels, same ŷ)."""
     net = net_for(name)
@@ -196,7 +219,8 @@ def test_roundtrip_bitexact(name, B, H, W, s):
     f = net(x, **kw)
     c = net.compress(x, **kw)
     d = net.decompress(c["strings"], c["shape"], **kw)
-    assert torch.equal(d["x_hat"], f["x_hat"])
+    if not torch.equal(d["x_hat"], f["x_hat"]):
+        _roundtrip_mismatch(net, x, c, d, f, kw, f"{name}_{B}x{H}x{W}")
 
 
 def test_lanes_do_not_change_bitstreams():
@@ -220,6 +244,36 @@ def test_lanes_do_not_change_bitstreams():
         assert ci["strings"][0][0] == outs[0][0][0][i] and ci["strings"][1][0] == outs[0][0][1][i]
 
 
+def test_reference_batched_y_stream(golden):
+    """The reference's B > 1 layout (mlicpp.py:215, 279-281 compress, 306-307 decompress): ONE y stream
+    for the batch.  compress(batch_stream=True) emits it -- its coder inputs equal the reference's own
+    list for this batch (fixture), its bytes are the native encoder's over that list -- and decompress()
+    decodes it to the same x_hat as the per-image streams and forward()."""
+    g = golden("batch_streams_MLICPP_S_3x128x192.npz")
+    net = net_for("MLICPP_S")
+    net.update()
+    x = torch.cat([synthetic.synth_image(128, 192, int(s_)) for s_ in g["seeds"]]).to(DEV)
+    c1 = net.compress(x)
+    per = [net.encoded_streams(b) for b in range(3)]
+    cb = net.compress(x, batch_stream=True)
+    assert len(cb["strings"][0]) == 1 and cb["strings"][1] == c1["strings"][1]
+    nph = 2 * net.slice_num
+    n_per = per[0][0].size // nph
+    sym = np.concatenate([per[b][0][k * n_per:(k + 1) * n_per] for k in range(nph) for b in range(3)])
+    idx = np.concatenate([per[b][1][k * n_per:(k + 1) * n_per] for k in range(nph) for b in range(3)])
+    rec = {"y_n": int(sym.size), "y_symbol_mismatch": int((sym != g["y_symbols"]).sum()),
+           "y_index_mismatch": int((idx != g["y_indexes"]).sum())}
+    PARITY["batch_stream_MLICPP_S_3x128x192"] = rec
+    assert rec["y_symbol_mismatch"] <= rec["y_n"] * 1e-3 and rec["y_index_mismatch"] <= rec["y_n"] * 1e-3, rec
+    gc = net.gaussian_conditional
+    tabs = (gc._quantized_cdf.cpu(), gc._cdf_length.cpu(), gc._offset.cpu())
+    assert cb["strings"][0][0] == entropy.rans_encode(sym, idx, *tabs)
+    d1 = net.decompress(c1["strings"], c1["shape"])
+    db = net.decompress(cb["strings"], cb["shape"])
+    assert torch.equal(db["x_hat"], d1["x_hat"])
+    assert torch.equal(db["x_hat"], net(x)["x_hat"])
+
+
 def test_1080p_parity_and_roundtrip():
     """BASELINE config 2 size: 1920x1088 MLICPP_L, bpp / PSNR vs the CPU oracle, and the
     size-independent round-trip invariant at full size."""
@@ -238,7 +292,8 @@ def test_1080p_parity_and_roundtrip():
     net.update()
     c = net.compress(x.to(DEV))
     d = net.decompress(c["strings"], c["shape"])
-    assert torch.equal(d["x_hat"], out["x_hat"])
+    if not torch.equal(d["x_hat"], out["x_hat"]):
+        _roundtrip_mismatch(net, x.to(DEV), c, d, out, {}, "1080p")
     nbytes = len(c["strings"][0][0]) + len(c["strings"][1][0])
     # the coder never costs more than the likelihood estimate (+ a small overhead); it can cost less
     # where escape (bypass) coding of outliers is cheaper than -log2 of the 1e-9 likelihood floor
@@ -338,7 +393,7 @@ def test_scale_index_sweep_bitexact(golden):
 
 
 RATES = [("MLICPP_L", 0, None), ("MLICPP_L", 2, None), ("MLICPP_L", 5, None), ("MLICPP_S", 1, None),
-         ("MLICPP_M_SMALL_DEC", 1, None), ("MLICPP_L_VBR", 2, 1)]
+         ("MLICPP_M_SMALL_DEC", 1, None), ("MLICPP_L_VBR", 2, 1), ("MLICPP_M_SMALL_DEC_VBR", 1, 2)]
 _RATE_NETS = {}
 
 
@@ -418,6 +473,30 @@ def test_bpp_lik_from_compress_equals_forward():
         assert abs(zb - ez) <= 1e-6 * max(1.0, ez) + 1e-3
 
 
+def _roundtrip_mismatch(net, xd, c, d, f, kw, tag):
+    """Diagnostics of a decompress-vs-forward x_hat mismatch, recorded in PARITY and raised: its extent
+    and first position, the fallback counters, and which side reproduces itself on a second call."""
+    dd = (d["x_hat"] - f["x_hat"]).abs()
+    bad = (dd > 0) | dd.isnan()
+    first = [int(v) for v in bad.nonzero()[0].tolist()] if bool(bad.any()) else None
+    fb = net.range_fallbacks()
+    f2 = net(xd, **kw)
+    d2 = net.decompress(c["strings"], c["shape"], **kw)
+    net.set_precision(0)
+    f0 = net(xd, **kw)
+    net.set_precision(2)
+    info = {"n_diff": int(bad.sum()), "max": float(dd.nan_to_num(nan=float("inf")).max()),
+            "first_bchw": first, "per_image": [int(bad[i].sum()) for i in range(dd.shape[0])],
+            "nan_forward": int(f["x_hat"].isnan().sum()), "nan_decompress": int(d["x_hat"].isnan().sum()),
+            "fallbacks": fb,
+            "forward_repeat_equal": torch.equal(f2["x_hat"], f["x_hat"]),
+            "decompress_repeat_equal": torch.equal(d2["x_hat"], d["x_hat"]),
+            "forward_is_fp32": torch.equal(f0["x_hat"], f["x_hat"]),
+            "decompress_is_fp32": torch.equal(f0["x_hat"], d["x_hat"])}
+    PARITY[f"roundtrip_mismatch_{tag}"] = info
+    raise AssertionError(info)
+
+
 def test_vbr_mixed_levels_batch_equals_per_image():
     """BASELINE config 5: one batch with a VBR level per image (mlicpp_vbr.py:137 `s`) equals one
     call per image, bit for bit, for forward, the bitstreams and the decoded images."""
@@ -430,21 +509,7 @@ def test_vbr_mixed_levels_batch_equals_per_image():
     c = net.compress(x, stage=2, s=levels)
     d = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
     if not torch.equal(d["x_hat"], f["x_hat"]):
-        # diagnostics for a mismatch: its extent, and which side reproduces itself on a second call
-        dd = (d["x_hat"] - f["x_hat"]).abs()
-        f2 = net(xd, stage=2, s=levels)
-        d2 = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
-        net.set_precision(0)
-        f0 = net(xd, stage=2, s=levels)
-        net.set_precision(2)
-        info = {"n_diff": int((dd > 0).sum()), "max": float(dd.max()),
-                "per_image": [int((dd[i] > 0).sum()) for i in range(dd.shape[0])],
-                "forward_repeat_equal": torch.equal(f2["x_hat"], f["x_hat"]),
-                "decompress_repeat_equal": torch.equal(d2["x_hat"], d["x_hat"]),
-                "forward_is_fp32": torch.equal(f0["x_hat"], f["x_hat"]),
-                "decompress_is_fp32": torch.equal(f0["x_hat"], d["x_hat"])}
-        PARITY["vbr_4k_roundtrip_mismatch"] = info
-        raise AssertionError(info)
+        _roundtrip_mismatch(net, x, c, d, f, {"stage": 2, "s": levels}, "vbr_mixed")
     for i, lv in enumerate(levels):
         fi = net(x[i:i + 1], stage=2, s=lv)
         assert torch.equal(fi["x_hat"], f["x_hat"][i:i + 1])
@@ -496,7 +561,8 @@ def test_4k_parity_and_roundtrip():
     net.update()
     c = net.compress(x.to(DEV))
     d = net.decompress(c["strings"], c["shape"])
-    assert torch.equal(d["x_hat"], out["x_hat"])
+    if not torch.equal(d["x_hat"], out["x_hat"]):
+        _roundtrip_mismatch(net, x.to(DEV), c, d, out, {}, "4k")
 
 
 @pytest.mark.parametrize("name", ["MLICPP_S", "MLICPP_M_SMALL_DEC"])
@@ -524,7 +590,8 @@ def test_config_size_parity_1080p(name):
     net.update()
     c = net.compress(x.to(DEV))
     d = net.decompress(c["strings"], c["shape"])
-    assert torch.equal(d["x_hat"], out["x_hat"])
+    if not torch.equal(d["x_hat"], out["x_hat"]):
+        _roundtrip_mismatch(net, x.to(DEV), c, d, out, {}, key)
 
 
 def test_vbr_4k_mixed_levels_vs_oracle_and_per_image():
@@ -541,21 +608,7 @@ def test_vbr_4k_mixed_levels_vs_oracle_and_per_image():
     c = net.compress(xd, stage=2, s=levels)
     d = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
     if not torch.equal(d["x_hat"], f["x_hat"]):
-        # diagnostics for a mismatch: its extent, and which side reproduces itself on a second call
-        dd = (d["x_hat"] - f["x_hat"]).abs()
-        f2 = net(xd, stage=2, s=levels)
-        d2 = net.decompress(c["strings"], c["shape"], stage=2, s=levels)
-        net.set_precision(0)
-        f0 = net(xd, stage=2, s=levels)
-        net.set_precision(2)
-        info = {"n_diff": int((dd > 0).sum()), "max": float(dd.max()),
-                "per_image": [int((dd[i] > 0).sum()) for i in range(dd.shape[0])],
-                "forward_repeat_equal": torch.equal(f2["x_hat"], f["x_hat"]),
-                "decompress_repeat_equal": torch.equal(d2["x_hat"], d["x_hat"]),
-                "forward_is_fp32": torch.equal(f0["x_hat"], f["x_hat"]),
-                "decompress_is_fp32": torch.equal(f0["x_hat"], d["x_hat"])}
-        PARITY["vbr_4k_roundtrip_mismatch"] = info
-        raise AssertionError(info)
+        _roundtrip_mismatch(net, xd, c, d, f, {"stage": 2, "s": levels}, "vbr_4k")
     for i, lv in enumerate(levels):
         fi = net(xd[i:i + 1], stage=2, s=lv)
         assert torch.equal(fi["x_hat"], f["x_hat"][i:i + 1])
@@ -619,6 +672,7 @@ def test_fp16_range_guard():
     f = net(x)
     torch.cuda.synchronize()
     assert torch.isfinite(f["x_hat"]).all()
+    assert net.range_fallbacks(reset=True) == {"forward_full": 1, "forward_gs": 0, "decompress_gs": 0}
     net.set_precision(0)
     f0 = net(x)
     assert torch.equal(f["x_hat"], f0["x_hat"])
@@ -629,9 +683,9 @@ def test_fp16_range_guard():
 
 
 def test_fp16_range_guard_synthesis_only():
-    """An activation beyond fp16 inside g_s only (a synthesis weight scaled up): forward() falls back to
-    exact fp32; compress() (no g_s) is unaffected; decompress() keeps the split-fp16 entropy model the
-    encoder used and re-runs only g_s in exact fp32 -- it decodes instead of refusing the stream."""
+    """An activation beyond fp16 inside g_s only (a synthesis weight scaled up): forward() and
+    decompress() both keep the split-fp16 entropy model and re-run g_s alone in exact fp32 (one
+    policy on both sides), so the round trip stays bit-exact; compress() (no g_s) is unaffected."""
     name, H, W = "MLICPP_S", 128, 128
     sd = synthetic.synth_state_dict(name, rate=1)
     k = "g_s.synthesis_transform.0.conv1.point_conv.weight"
@@ -641,17 +695,19 @@ def test_fp16_range_guard_synthesis_only():
     net = net.to(DEV).eval()
     x = synthetic.synth_image(H, W, 4).to(DEV)
     f = net(x)
+    assert net.range_fallbacks(reset=True) == {"forward_full": 0, "forward_gs": 1, "decompress_gs": 0}
     net.set_precision(0)
     f0 = net(x)
     net.set_precision(2)
-    assert torch.isfinite(f["x_hat"]).all() and torch.equal(f["x_hat"], f0["x_hat"])
+    assert torch.isfinite(f["x_hat"]).all()
     net.update()
     c = net.compress(x)
     d = net.decompress(c["strings"], c["shape"])
-    xd, xf = d["x_hat"].double(), f["x_hat"].double()
-    assert torch.isfinite(xd).all()
+    assert net.range_fallbacks(reset=True) == {"forward_full": 0, "forward_gs": 0, "decompress_gs": 1}
+    assert torch.equal(d["x_hat"], f["x_hat"])
+    xd, xf = d["x_hat"].double(), f0["x_hat"].double()
     rel = float((xd - xf).abs().mean() / xf.abs().mean().clamp_min(1e-12))
-    PARITY["range_guard_gs_only"] = {"decode_vs_fp32_forward_mean_rel": rel}
+    PARITY["range_guard_gs_only"] = {"decode_vs_all_fp32_forward_mean_rel": rel}
     assert rel <= 1e-3, rel
     # and the same stream decoded again gives the same image (the fallback is deterministic)
     d2 = net.decompress(c["strings"], c["shape"])

@@ -80,7 +80,8 @@ def test_module_vectors(golden):
 FWD = [("MLICPP_L", 128, 192, None), ("MLICPP_L", 128, 128, None), ("MLICPP_S", 128, 128, None),
        ("MLICPP_S2", 128, 128, None), ("MLICPP_M", 128, 128, None), ("MLICPP_M_SMALL_DEC", 128, 128, None),
        ("MLICPP_L_VBR", 128, 128, 0), ("MLICPP_L_VBR", 128, 128, 3), ("MLICPP_L_VBR", 128, 128, 5),
-       ("MLICPP_S_VBR", 128, 128, 0), ("MLICPP_S_VBR", 128, 128, 3), ("MLICPP_S_VBR", 128, 128, 5)]
+       ("MLICPP_S_VBR", 128, 128, 0), ("MLICPP_S_VBR", 128, 128, 3), ("MLICPP_S_VBR", 128, 128, 5),
+       ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 0), ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 3)]
 
 
 @pytest.mark.parametrize("name,H,W,s", FWD)
@@ -107,7 +108,8 @@ def test_forward_matches_reference(golden, name, H, W, s):
 @pytest.mark.parametrize("name,H,W,s,img", [("MLICPP_L", 128, 192, None, 0), ("MLICPP_S", 128, 128, None, 0),
                                             ("MLICPP_M_SMALL_DEC", 128, 128, None, 0), ("MLICPP_S_VBR", 128, 128, 0, 0),
                                             ("MLICPP_S_VBR", 128, 128, 3, 0), ("MLICPP_S_VBR", 128, 128, 5, 0),
-                                            ("MLICPP_S_VBR", 192, 256, 1, 3)])
+                                            ("MLICPP_S_VBR", 192, 256, 1, 3), ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 0, 0),
+                                            ("MLICPP_M_SMALL_DEC_VBR", 128, 128, 3, 0)])
 def test_compress_streams_match_reference(golden, name, H, W, s, img):
     """Coder inputs (y symbols / indexes, z symbols) vs the reference's.  VBR: the fixture holds the
     values a consistent codec codes, taken from the reference forward itself (oracle/gen_golden.py
@@ -133,7 +135,7 @@ def test_compress_streams_match_reference(golden, name, H, W, s, img):
 # realistic-rate weight sets (synthetic.RATE_LAMBDAS stand-ins, 0.06-0.9 bpp): forward and the exact
 # coder inputs, oracle vs the reference (oracle/gen_golden.py "rates")
 RATES = [("MLICPP_L", 0, None), ("MLICPP_L", 2, None), ("MLICPP_L", 5, None), ("MLICPP_S", 1, None),
-         ("MLICPP_M_SMALL_DEC", 1, None), ("MLICPP_L_VBR", 2, 1)]
+         ("MLICPP_M_SMALL_DEC", 1, None), ("MLICPP_L_VBR", 2, 1), ("MLICPP_M_SMALL_DEC_VBR", 1, 2)]
 
 
 @pytest.mark.parametrize("name,rate,s", RATES)
@@ -151,9 +153,26 @@ def test_rate_sets_match_reference(golden, name, rate, s):
     assert abs(ref.bpp_from_likelihoods(yl, zl, H * W) - float(g["bpp"])) < 1e-4
     close(out["x_hat"], g["x_hat"], rtol=1e-4, atol=1e-4)
     if "y_symbols" in g.files:
-        st = m.compress_streams(x)
+        st = m.compress_streams(x, **({} if s is None else {"s": s}))
         sym = torch.cat([p[0].reshape(-1) for p in st["phases"]]).numpy()
         idx = torch.cat([p[1].reshape(-1) for p in st["phases"]]).numpy()
         assert np.array_equal(st["z_symbols"].numpy(), g["z_symbols"])
         assert np.array_equal(idx, g["y_indexes"])
         assert np.array_equal(sym, g["y_symbols"])
+
+
+def test_reference_batch_stream_order(golden):
+    """The reference codes a B > 1 batch into ONE y stream (mlicpp.py:215, 279-281): its coder inputs are
+    each image's phase streams interleaved phase-major, image-minor (the order mlic_batch_stream codes).
+    Checked against the reference's own list for a 3-image batch (oracle/gen_golden.py gen_batch_streams)."""
+    g = golden("batch_streams_MLICPP_S_3x128x192.npz")
+    assert int(g["n_y_strings"]) == 1 and int(g["n_z_strings"]) == 3
+    name = "MLICPP_S"
+    m = ref.RefMLIC(name, synthetic.synth_state_dict(name, 0))
+    per = [m.compress_streams(synthetic.synth_image(128, 192, int(s_))) for s_ in g["seeds"]]
+    sym = np.concatenate([per[b]["phases"][k][0].reshape(-1).numpy()
+                          for k in range(len(per[0]["phases"])) for b in range(len(per))])
+    idx = np.concatenate([per[b]["phases"][k][1].reshape(-1).numpy()
+                          for k in range(len(per[0]["phases"])) for b in range(len(per))])
+    assert np.array_equal(idx, g["y_indexes"])
+    assert np.array_equal(sym, g["y_symbols"])
