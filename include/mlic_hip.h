@@ -97,6 +97,11 @@ int mlic_set_synthesis_precision(mlic_model* m, int mode);
 /* test switch: fill every workspace block with NaN (0xFF bytes) when it is handed out, so a kernel
  * reading memory its producer never wrote fails visibly (also $MLIC_POISON=1).  Off by default. */
 int mlic_set_poison(mlic_model* m, int on);
+/* process-wide kernel A/B switches (tests, micro-benchmarks): "x4_halo" = the conv_x4 kernel's
+ * halo-staged B operand for K x K stride-1 convs (1 on, 0 off, -1 default = $MLIC_X4_HALO or on);
+ * "linatt_fused" = the linear attention's one-launch context + its output written straight into the
+ * reprojection conv's packed operand ($MLIC_LINATT_FUSED) */
+int mlic_set_kernel_option(const char* name, int value);
 /* fp16 range-guard fallbacks taken since the last reset (each changes the arithmetic of one call):
  * forward re-run whole in exact fp32 (the entropy model left fp16's range; compress refuses such an
  * input), forward's g_s alone, decompress's g_s alone (the same policy on both sides, so

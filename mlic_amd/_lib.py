@@ -46,6 +46,7 @@ def _sig(lib):
         "mlic_set_precision": [p, i],
         "mlic_set_synthesis_precision": [p, i],
         "mlic_set_poison": [p, i],
+        "mlic_set_kernel_option": [C.c_char_p, i],
         "mlic_batch_stream": [p, i, i, p, sz, P(sz)],
         "mlic_decompress_batch_stream": [p, p, p, sz, P(p), P(sz), i, i, i, p, p],
         "mlic_range_fallbacks": [p, P(i64), P(i64), P(i64), i],

@@ -217,6 +217,16 @@ int mlic_set_precision(mlic_model* m, int precision) {
   });
 }
 
+int mlic_set_kernel_option(const char* name, int value) {
+  return guard([&] {
+    MLIC_CHECK(name, "null option name");
+    const std::string n = name;
+    if (n == "x4_halo") x4_set_halo(value);
+    else if (n == "linatt_fused") linatt_set_fused(value);
+    else throw Error("mlic: unknown kernel option " + n);
+  });
+}
+
 int mlic_set_poison(mlic_model* m, int on) {
   return guard([&] { impl(m).set_poison(on != 0); });
 }

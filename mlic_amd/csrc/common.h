@@ -104,6 +104,27 @@ struct ConvParams {
 // Encoder and decoder run the same kernels, so bit-reproducibility is unaffected.
 __device__ __forceinline__ float softmax_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 
+// linear attention: the channel softmax of one pixel's query (context.py:181, 236), in registers; shared by attn_apply and
+// the fused pack (linatt_pack_kernel), which must produce the same bits
+template <int HD>
+__device__ __forceinline__ void query_softmax(const float* qp, int HW, float (&q)[HD]) {
+  float mx = -3.0e38f;
+#pragma unroll
+  for (int c = 0; c < HD; ++c) {
+    q[c] = qp[(int64_t)c * HW];
+    mx = fmaxf(mx, q[c]);
+  }
+  float sum = 0.0f;
+#pragma unroll
+  for (int c = 0; c < HD; ++c) {
+    q[c] = softmax_exp(q[c] - mx);
+    sum += q[c];
+  }
+  const float inv = 1.0f / sum;
+#pragma unroll
+  for (int c = 0; c < HD; ++c) q[c] *= inv;
+}
+
 __device__ __forceinline__ bool f16_unsafe(float v) { return (__float_as_uint(v) & 0x7fffffffu) >= 0x477ff000u; }
 __device__ __forceinline__ void range_report(int* flag, bool bad) {
   if (bad && flag) atomicOr(flag, 1);

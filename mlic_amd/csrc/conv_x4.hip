@@ -67,7 +67,12 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 // DIR (K = 1, split form): no packed copy -- the B rows are built from the fp32 NCHW input segments
 // in registers (lane = pixel, 16 channels per thread, split hi / lo with the pack kernel's RNE
 // conversions) and written into the same swizzled LDS image; the fp16 range check rides along
-template <int K, int BM, bool RS, bool HI, bool DIR = false>
+// HALO (K = 3, 5, stride 1; register-staged): the B operand of a 32-channel chunk is staged ONCE per
+// chunk as the tile's (8 + K - 1) x (32 + K - 1) halo of packed lines (K = 3: 340 lines, 43.5 KB), and
+// every tap reads its fragments from that image at the tap's (ky, kx) shift -- instead of 256 lines
+// per tap (K^2 x the L2 -> LDS bytes and VMEM instructions for B).  The next chunk's halo is loaded one
+// piece per thread per step, spread over the current chunk's taps, into the other halo slot.
+template <int K, int BM, bool RS, bool HI, bool DIR = false, bool HALO = false>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
                                                       const _Float16* __restrict__ wx, int nchunk, int H, int W,
                                                       int abl, int nsplit) {
@@ -83,10 +88,13 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   constexpr int WR = 16 * TM;             // Cout rows per wave
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
   constexpr int NAB = RS ? 2 : 3;  // A ring slots
-  constexpr int B_OFF = NAB * A_BYTES, LDS = NAB * A_BYTES + 2 * B_BYTES;
+  constexpr int HR = TR + K - 1, HC = TC + K - 1, HLINES = HR * HC;  // HALO: the chunk's halo image
+  constexpr int BSLOT = HALO ? HLINES * ROWB : B_BYTES;
+  constexpr int B_OFF = NAB * A_BYTES, LDS = NAB * A_BYTES + 2 * BSLOT;
   constexpr int NA = A_BYTES / 1024 / 8;  // 1 KB glds instructions per wave for A
   constexpr int NB = B_BYTES / 1024 / 8;  // ... for B
   static_assert(NA >= 1 && NB == 4 && LDS <= 160 * 1024, "x4 tile");
+  static_assert(!HALO || (RS && !DIR && K > 1), "x4 halo: register-staged K x K only");
   __shared__ __attribute__((aligned(1024))) char sm[LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -111,7 +119,9 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
   // its raw partial sums into plane `split` of the partial buffer (P carries that layout, no epilogue)
   const int b = blockIdx.z % P.B, split = blockIdx.z / P.B;
   const int nsteps = nchunk * KK;
-  const int s0 = split * nsteps / nsplit, s1 = (split + 1) * nsteps / nsplit;
+  // (HALO: the K ranges start and end on chunk boundaries, so every chunk a block runs is whole)
+  const int s0 = HALO ? split * nchunk / nsplit * KK : split * nsteps / nsplit;
+  const int s1 = HALO ? (split + 1) * nchunk / nsplit * KK : (split + 1) * nsteps / nsplit;
   if (nsplit > 1) P.out += (int64_t)split * P.B * P.out_bs;
 
   // per-lane DMA sources.  B: instruction i of this wave moves pixels n = (wave*NB + i)*8 + lane/8,
@@ -156,7 +166,24 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     // wave + 8 i (BM 96 has 12: waves 0-3 take two)
     constexpr int NPA = A_BYTES / 1024, NAR = (NPA + 7) / 8;
     const _Float16* asrc_rs = wx + ((int64_t)ct * nsteps * BM) * ROWH + wave * 512 + lane * 8;
-    u32x4 rb[DIR ? 1 : NB], ra[NAR];
+    u32x4 rb[(DIR || HALO) ? 1 : NB], ra[NAR];
+    // HALO: pieces (16 bytes = one granule of one halo line) per thread per chunk; piece q of thread
+    // tid is q * X4T + tid: line (q * X4T + tid) >> 3, logical granule & 7
+    constexpr int NPH = (HLINES * 8 + X4T - 1) / X4T;
+    static_assert(!HALO || NPH + 1 <= KK, "x4 halo: the next chunk's pieces must land within the chunk");
+    u32x4 hb;
+    const _Float16* himg = act + (int64_t)b * nchunk * plane;
+    auto hsrc = [&](int q) __attribute__((always_inline)) {  // packed line of halo piece q (clamped)
+      const int id = q * X4T + tid, line = min(id >> 3, HLINES - 1);
+      const int hr = line / HC, hc = line - hr * HC;
+      const int y = min(oy0 + hr, Hp - 1), x = min(ox0 + hc, Wp - 1);
+      return ((int64_t)y * Wp + x) * ROWH + (id & 7) * 8;
+    };
+    auto hdst = [&](int q, int slot) __attribute__((always_inline)) {
+      const int id = q * X4T + tid, line = id >> 3;
+      return sm + B_OFF + slot * BSLOT + line * ROWB + (((id & 7) ^ swz(line)) << 4);
+    };
+    auto hvalid = [&](int q) __attribute__((always_inline)) { return q * X4T + tid < HLINES * 8; };
     // DIR: tile pixel dn = 64 (wave & 3) + lane (flat pixel dp, clamped into the image: the ragged
     // tail's outputs are discarded), channels dch .. dch + 15 of the step's 32-channel chunk
     float rv[DIR ? 16 : 1];
@@ -196,7 +223,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
 #pragma unroll
           for (int j = 0; j < 16; ++j) rv[j] = j < nval ? src[(int64_t)j * npix] : 0.0f;
         }
-      } else {
+      } else if constexpr (!HALO) {
         const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
 #pragma unroll
         for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const u32x4*>(bsrc[i] + d);
@@ -229,7 +256,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           *reinterpret_cast<half8*>(row + (((g0 + q) ^ sw) << 4)) = h;
           *reinterpret_cast<half8*>(row + (((g0 + q + 4) ^ sw) << 4)) = l;
         }
-      } else {
+      } else if constexpr (!HALO) {
 #pragma unroll
         for (int i = 0; i < NB; ++i)
           *reinterpret_cast<u32x4*>(sm + B_OFF + (st & 1) * B_BYTES + (wave * NB + i) * 1024 + lane * 16) = rb[i];
@@ -242,7 +269,19 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     // step s's MFMAs on LDS slot s & 1 (fragment reads one pixel group ahead)
     auto mfma_step = [&](int s) {
       const char* As = sm + (s & 1) * A_BYTES;
-      const char* Bs = sm + B_OFF + (s & 1) * B_BYTES;
+      const char* Bs;
+      int tapoff = 0;  // HALO: the tap's (ky, kx) shift in the halo image, in lines
+      if constexpr (HALO) {
+        const int cc = s / KK, tap = s - cc * KK, ky = tap / K;
+        Bs = sm + B_OFF + (cc & 1) * BSLOT;
+        tapoff = ky * HC + (tap - ky * K);
+      } else {
+        Bs = sm + B_OFF + (s & 1) * B_BYTES;
+      }
+      // B row of tile pixel n: the pixel's own line, or its halo line at the tap's shift
+      auto brow = [&](int n) __attribute__((always_inline)) {
+        return HALO ? (n / TC) * HC + (n % TC) + tapoff : n;
+      };
       half8 ah[TM], al[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -251,12 +290,12 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
         al[i] = lds_frag(As, row, G + 4);
       }
       half8 bh[2], bl[2];
-      bh[0] = lds_frag(Bs, wn * WN + l16, G);
-      bl[0] = lds_frag(Bs, wn * WN + l16, G + 4);
+      bh[0] = lds_frag(Bs, brow(wn * WN + l16), G);
+      bl[0] = lds_frag(Bs, brow(wn * WN + l16), G + 4);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if (j + 1 < TN) {
-          const int n = wn * WN + (j + 1) * 16 + l16;
+          const int n = brow(wn * WN + (j + 1) * 16 + l16);
           bh[(j + 1) & 1] = lds_frag(Bs, n, G);
           bl[(j + 1) & 1] = lds_frag(Bs, n, G + 4);
         }
@@ -280,8 +319,19 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
         }
       }
     };
-    gload(s0);
-    lstore(s0);
+    if (HALO && s0 < s1) {  // the first chunk's halo image, whole
+      const int c0 = s0 / KK;
+#pragma unroll
+      for (int q = 0; q < NPH; ++q)
+        if (hvalid(q)) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(himg + c0 * plane + hsrc(q));
+          *reinterpret_cast<u32x4*>(hdst(q, c0 & 1)) = v;
+        }
+    }
+    if (s0 < s1) {
+      gload(s0);
+      lstore(s0);
+    }
     if (s0 + 1 < s1) gload(s0 + 1);
     for (int s = s0; s < s1; ++s) {
       // this wave's stores of step s done; barrier: every wave's too, and step s-1's reads of the
@@ -290,6 +340,16 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (s + 1 < s1) lstore(s + 1);
+      if constexpr (HALO) {
+        // the next chunk's halo: piece j - 1 stored and piece j loaded at local step j (the slot
+        // (cc + 1) & 1 was last read in chunk cc - 1, before this chunk's first barrier; its last
+        // piece lands at step NPH <= KK - 1, before chunk cc + 1's first barrier)
+        const int cc = s / KK, j = s - cc * KK;
+        if ((cc + 1) * KK < s1) {
+          if (j >= 1 && j <= NPH && hvalid(j - 1)) *reinterpret_cast<u32x4*>(hdst(j - 1, (cc + 1) & 1)) = hb;
+          if (j < NPH && hvalid(j)) hb = *reinterpret_cast<const u32x4*>(himg + (cc + 1) * plane + hsrc(j));
+        }
+      }
       if (s + 2 < s1) gload(s + 2);
       mfma_step(s);
     }
@@ -509,6 +569,107 @@ __global__ __launch_bounds__(256) void x4_pack_act_kernel(X4Pack Q) {
   range_report(Q.rflag, bad);
 }
 
+// ---------------------------------------------------------------------------------------------
+// the linear attention's output (context.py:181-187, 236-239: att = ctx^T . softmax_c(q) per pixel)
+// computed straight into the packed split layout of the reprojection conv that consumes it: one pass
+// over Q instead of attn_apply's fp32 att write + x4_pack_act's read.  Same op sequence as attn_apply
+// (query_softmax, then one fma chain over c per output channel) and the pack's split, so the packed
+// halves equal x4_pack_act(attn_apply(...)) bit for bit.  grid (ceil(Hp*Wp / 64), nchunk, B), 256
+// threads: lane = position, wave g = channels 8g .. 8g + 7 of the chunk (one head for hd = 32; the
+// chunk's two heads for hd = 16).  qmask: queries at non-anchor positions only (anchors output 0).
+struct LinAttPack {
+  const float* Q;
+  int64_t q_bs;
+  const float* ctx;  // [B][heads][hd][hd]
+  int heads, H, W, pad, nchunk, qmask;
+  _Float16* dst;
+  int* rflag;
+};
+
+template <int HD>
+__global__ __launch_bounds__(256) void linatt_pack_kernel(LinAttPack A) {
+  constexpr int HPC = 32 / HD;  // heads per 32-channel chunk
+  __shared__ __attribute__((aligned(16))) float cs[HPC * HD * HD];
+  const int Hp = A.H + 2 * A.pad, Wp = A.W + 2 * A.pad, HW = A.H * A.W;
+  const int cc = blockIdx.y, b = blockIdx.z;
+  const float* cb = A.ctx + ((int64_t)b * A.heads + cc * HPC) * HD * HD;
+  for (int i = threadIdx.x; i < HPC * HD * HD; i += 256) cs[i] = cb[i];
+  __syncthreads();
+  const int pos = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int y = pos / Wp - A.pad, x = pos % Wp - A.pad;
+  const bool inb = pos < Hp * Wp && y >= 0 && y < A.H && x >= 0 && x < A.W;
+  const int hl = (8 * g) / HD, d0 = (8 * g) % HD;  // head within the chunk, first output channel
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.0f;
+  if (inb && !(A.qmask && is_anchor(y, x))) {
+    float q[HD];
+    query_softmax<HD>(A.Q + (int64_t)b * A.q_bs + (int64_t)(cc * HPC + hl) * HD * HW + (int64_t)y * A.W + x, HW, q);
+    const float* w = cs + hl * HD * HD + d0;
+#pragma unroll
+    for (int c = 0; c < HD; ++c) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + c * HD), w1 = *reinterpret_cast<const float4*>(w + c * HD + 4);
+      a[0] = fmaf(w0.x, q[c], a[0]);
+      a[1] = fmaf(w0.y, q[c], a[1]);
+      a[2] = fmaf(w0.z, q[c], a[2]);
+      a[3] = fmaf(w0.w, q[c], a[3]);
+      a[4] = fmaf(w1.x, q[c], a[4]);
+      a[5] = fmaf(w1.y, q[c], a[5]);
+      a[6] = fmaf(w1.z, q[c], a[6]);
+      a[7] = fmaf(w1.w, q[c], a[7]);
+    }
+  }
+  bool bad = false;
+  half8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 hv = (_Float16)a[j];
+    h[j] = hv;
+    l[j] = (_Float16)(a[j] - (float)hv);
+    bad |= f16_unsafe(a[j]);
+  }
+  // x4_pack_act_kernel's store: the block's 64 lines assembled in LDS, whole lines per instruction
+  constexpr int SP = ROWH + 8;
+  __shared__ __attribute__((aligned(16))) _Float16 stg[64 * SP];
+  const int lane = threadIdx.x & 63;
+  *reinterpret_cast<half8*>(stg + lane * SP + 8 * g) = h;
+  *reinterpret_cast<half8*>(stg + lane * SP + 32 + 8 * g) = l;
+  __syncthreads();
+  const int nlines = min(64, Hp * Wp - (int)blockIdx.x * 64);
+  _Float16* d = A.dst + (((int64_t)b * A.nchunk + cc) * Hp * Wp + (int64_t)blockIdx.x * 64) * ROWH;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = k * 256 + threadIdx.x;
+    if (q / 8 < nlines)
+      *reinterpret_cast<half8*>(d + q * 8) = *reinterpret_cast<const half8*>(stg + (q / 8) * SP + (q % 8) * 8);
+  }
+  range_report(A.rflag, bad);
+}
+
+void linatt_pack(const float* Q, int64_t q_bs, const float* ctx, int heads, int hd, int qmask, const ConvParams& P,
+                 _Float16* dst, hipStream_t st) {
+  MLIC_CHECK((hd == 16 || hd == 32) && P.Cin == heads * hd && P.Cin % 32 == 0 && P.K > 1 && P.stride == 1,
+             "linatt_pack: shape");
+  LinAttPack A{};
+  A.Q = Q;
+  A.q_bs = q_bs;
+  A.ctx = ctx;
+  A.heads = heads;
+  A.H = P.H;
+  A.W = P.W;
+  A.pad = P.K / 2;
+  A.nchunk = P.Cin / 32;
+  A.qmask = qmask;
+  A.dst = dst;
+  A.rflag = P.rflag;
+  const int npos = (A.H + 2 * A.pad) * (A.W + 2 * A.pad);
+  const dim3 grid((npos + 63) / 64, A.nchunk, P.B);
+  if (hd == 16) hipLaunchKernelGGL(linatt_pack_kernel<16>, grid, dim3(256), 0, st, A);
+  else hipLaunchKernelGGL(linatt_pack_kernel<32>, grid, dim3(256), 0, st, A);
+  HIP_OK(hipGetLastError());
+}
+
 // weights: hi/lo [Cout][KK][cin_pad] -> [ct][step = chunk*KK + tap][BM rows][64 halves], swizzled;
 // hi: the reduced-precision image, chunks of 64 channels of hi only (channels >= cin_pad are zeros)
 __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _Float16* __restrict__ wl,
@@ -639,6 +800,28 @@ static bool x4_rs() {
   return on;
 }
 
+// the halo-staged B operand (conv_x4_kernel HALO) for a packed K x K stride-1 conv whose LDS images fit;
+// $MLIC_X4_HALO=0: B staged per tap (A/B switch)
+static int g_x4_halo = -1;  // mlic_set_kernel_option("x4_halo"): -1 = $MLIC_X4_HALO / default on
+void x4_set_halo(int on) { g_x4_halo = on; }
+static bool x4_halo_on() {
+  static const bool env = [] {
+    const char* e = std::getenv("MLIC_X4_HALO");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return g_x4_halo < 0 ? env : g_x4_halo != 0;
+}
+template <int K, int BM>
+constexpr bool x4_halo_fits() {
+  constexpr int a = 2 * BM * ROWB, h = 2 * (TR + K - 1) * (TC + K - 1) * ROWB;
+  return K > 1 && a + h <= 160 * 1024;
+}
+static bool x4_halo(const ConvParams& P, bool hi) {
+  if (!x4_halo_on() || P.K == 1 || P.stride != 1) return false;
+  const int bm = x4_bm(P.Cout);
+  return 2 * bm * ROWB + 2 * (TR + P.K - 1) * (TC + P.K - 1) * ROWB <= 160 * 1024;
+}
+
 // $MLIC_X4_DIRECT=0: 1x1 layers read the packed copy too (A/B switch)
 bool x4_direct_ok(const ConvParams& P, bool hi) {
   static const bool on = [] {
@@ -662,10 +845,18 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
   if (K == 1 && !act)
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false, K == 1>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W,
                        abl, nsplit);
-  else if (hi)
+  else if (hi && x4_halo(P, hi)) {
+    if constexpr (x4_halo_fits<K, BM>())
+      hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, true, false, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk,
+                         H, W, abl, nsplit);
+  } else if (hi)
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
                        nsplit);
-  else if (x4_rs())
+  else if (x4_rs() && x4_halo(P, hi)) {
+    if constexpr (x4_halo_fits<K, BM>())
+      hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false, false, true>), grid, dim3(X4T), 0, st, P, act, wx, nchunk,
+                         H, W, abl, nsplit);
+  } else if (x4_rs())
     hipLaunchKernelGGL((conv_x4_kernel<K, BM, true, false>), grid, dim3(X4T), 0, st, P, act, wx, nchunk, H, W, abl,
                        nsplit);
   else if constexpr (BM != 192 && BM != 96 && BM != 224)  // (the DMA path's counted waits: 1, 2 or 4 A pieces per wave)
@@ -691,7 +882,9 @@ int x4_splitk(const ConvParams& P, int cin_pad, bool hi) {
   const int tiles = ((P.Cout + x4_bm(P.Cout) - 1) / x4_bm(P.Cout)) * ((W + TC - 1) / TC) * ((H + TR - 1) / TR);
   const int nsteps = x4_nchunk(cin_pad, hi) * P.K * P.K;
   if (tiles > 48 || nsteps < 48) return 1;
-  return std::min(4, nsteps / 24);
+  const int s = std::min(4, nsteps / 24);
+  // the halo form splits on chunk boundaries: no more splits than chunks
+  return x4_halo(P, hi) ? std::max(1, std::min(s, x4_nchunk(cin_pad, hi))) : s;
 }
 
 int64_t x4_part_bytes(const ConvParams& P, int cin_pad, bool hi) {

@@ -567,7 +567,7 @@ void Model::conv_pair(const std::vector<View>& ins, const ConvW& w1, const View&
 }
 
 // packed: the input already in x4's split layout (conv_pair); the impl is then necessarily x4
-void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi) {
+void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi, bool split) {
   const ConvWeights cw{w.w, w.wh, w.wl, w.cin_pad, w.wx4, w.wexp};
   const int impl = packed ? (hi ? CONV_X4H : CONV_X4) : conv_select(P, cw, prec());
   const double outn = (double)P.B * w.Cout * P.Ho * P.Wo;
@@ -582,8 +582,13 @@ void Model::run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed
     tag = w.name + sh;
   }
   if (packed) {
+    // split: the few-tile split-K path of conv_run (x4_splitk), for a packed operand made elsewhere
+    const int64_t pb = split ? x4_part_bytes(P, w.cin_pad, hi) : 0;
+    const size_t m = L().arena.mark();
+    float* part = pb > 0 ? L().arena.alloc((pb + 3) / 4) : nullptr;
     timed(conv_prof_cat(impl, P), flops, bytes,
-          [&] { conv_x4_forward(P, packed, hi ? w.wx4h : w.wx4, w.cin_pad, L().st, nullptr, hi); }, tag);
+          [&] { conv_x4_forward(P, packed, hi ? w.wx4h : w.wx4, w.cin_pad, L().st, part, hi); }, tag);
+    L().arena.release(m);
     return;
   }
   const int64_t wsb = conv_ws_bytes(impl, P, cw);
@@ -999,18 +1004,9 @@ View Model::inter_context(const View& x, int i) {
   View q = qkv_branch(x, p + ".queries");
   View k = qkv_branch(x, p + ".keys");
   View v = qkv_branch(x, p + ".values");
-  View att = alloc(D, H, W);
-  const int nsplit = ctx_splits(HW);
-  float* part = L().arena.alloc(linear_attention_part_floats(heads, hd, L().B, nsplit));
-  float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
-  // algorithmic bytes: k, v, q read once, the output written once
-  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 4.0, [&] {
-    linear_attention(k.p, k.bs, v.p, v.bs, q.p, q.bs, att.p, att.bs, part, ctx, heads, hd, H, W, L().B, nsplit, 0, 0,
-                     L().st);
-  }, p + ".attn");
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
-  conv({att}, rp, 1, 2, a, EPI_NONE);
+  linatt_reproject(k, v, q, heads, hd, 0, 0, rp, a, p + ".attn");
   View m1 = conv1x1(a, p + ".mlp.0", 1, EPI_GELU);
   View m2 = alloc(m1.C, H, W);
   dw({m1}, dww(p + ".mlp.2"), 1, m2, true);
@@ -1018,6 +1014,54 @@ View Model::inter_context(const View& x, int i) {
   conv({m2}, cw(p + ".mlp.4"), 1, 0, out, EPI_NONE, nullptr, &s);
   L().arena.release(m);
   return out;
+}
+
+// $MLIC_LINATT_FUSED=0: the three-launch linear attention + fp32 att + the reprojection's own pack (A/B)
+static int g_linatt_fused = -1;  // mlic_set_kernel_option("linatt_fused"): -1 = the environment / on
+void linatt_set_fused(int on) { g_linatt_fused = on; }
+static bool linatt_fused_on() {
+  static const bool env = [] {
+    const char* e = std::getenv("MLIC_LINATT_FUSED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return g_linatt_fused < 0 ? env : g_linatt_fused != 0;
+}
+
+// the linear attention and the 5x5 reprojection conv that consumes it (context.py:180-190, 235-241).
+// Fused (default, when the reprojection runs on conv_x4): ctx in one launch (partials + in-launch
+// combine), then ctx^T . softmax_c(q) written straight into the conv's packed split operand -- the
+// fp32 attention map is never stored.  Bit-identical to the unfused form (linatt_pack_kernel).
+void Model::linatt_reproject(const View& k, const View& v, const View& q, int heads, int hd, int kmask, int qmask,
+                             const ConvW& rp, const View& a, const std::string& tag) {
+  const int H = q.H, W = q.W, HW = H * W, D = heads * hd, B = L().B;
+  const int nsplit = ctx_splits(HW);
+  const size_t m = L().arena.mark();
+  float* part = L().arena.alloc(linear_attention_part_floats(heads, hd, B, nsplit));
+  float* ctx = L().arena.alloc((int64_t)B * heads * hd * hd);
+  // algorithmic bytes: k, v, q read once, the attention written once
+  const double fl = (double)B * HW * D * hd * 4.0, by = 4.0 * B * HW * D * 4.0;
+  const View geo{nullptr, D, H, W, (int64_t)D * HW};  // geometry only: the fused conv reads its packed operand
+  const ConvParams P = conv_params({geo}, rp, 1, 2, a, EPI_NONE, nullptr, nullptr);
+  const ConvWeights cwt{rp.w, rp.wh, rp.wl, rp.cin_pad, rp.wx4, rp.wexp};
+  if (linatt_fused_on() && rp.cin_pad == D && D % 32 == 0 && conv_select(P, cwt, prec()) == CONV_X4) {
+    unsigned* cnt = reinterpret_cast<unsigned*>(L().arena.alloc((int64_t)B * heads));
+    timed(PCAT_LINATT, fl * 0.5, 4.0 * B * HW * D * 2.0, [&] {
+      linear_attention_ctx(k.p, k.bs, v.p, v.bs, part, ctx, cnt, heads, hd, H, W, B, nsplit, kmask, L().st);
+    }, tag);
+    _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((2 * x4_act_halves(P, rp.cin_pad) + 3) / 4));
+    timed(PCAT_LINATT, fl * 0.5, 4.0 * B * HW * D * 2.0, [&] {
+      linatt_pack(q.p, q.bs, ctx, heads, hd, qmask, P, act, L().st);
+    }, tag + ".pack");
+    run_conv(P, rp, act, false, true);
+  } else {
+    View att = alloc(D, H, W);
+    timed(PCAT_LINATT, fl, by, [&] {
+      linear_attention(k.p, k.bs, v.p, v.bs, q.p, q.bs, att.p, att.bs, part, ctx, heads, hd, H, W, B, nsplit, kmask, qmask,
+                       L().st);
+    }, tag);
+    conv({att}, rp, 1, 2, a, EPI_NONE);
+  }
+  L().arena.release(m);
 }
 
 // context.py:140-193 LinearGlobalIntraContext: q from non-anchor cells of x1, k from anchor cells of
@@ -1037,17 +1081,9 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
   View q = qkv_branch(x1n, p + ".queries");
   View k = qkv_branch(x1a, p + ".keys");
   View v = qkv_branch(x2, p + ".values");
-  View att = alloc(D, H, W);
-  const int nsplit = ctx_splits(HW);
-  float* part = L().arena.alloc(linear_attention_part_floats(heads, hd, L().B, nsplit));
-  float* ctx = L().arena.alloc((int64_t)L().B * heads * hd * hd);
-  timed(PCAT_LINATT, (double)L().B * HW * D * hd * 4.0, 4.0 * L().B * HW * D * 4.0, [&] {
-    linear_attention(k.p, k.bs, v.p, v.bs, q.p, q.bs, att.p, att.bs, part, ctx, heads, hd, H, W, L().B, nsplit, 1, 2,
-                     L().st);
-  }, p + ".attn");
   const ConvW& rp = cw(p + ".reprojection");
   View a = alloc(rp.Cout, H, W);
-  conv({att}, rp, 1, 2, a, EPI_NONE);
+  linatt_reproject(k, v, q, heads, hd, 1, 2, rp, a, p + ".attn");
   View m1 = conv1x1(a, p + ".mlp.0", 1, EPI_GELU);
   View m2 = alloc(m1.C, H, W);
   dw({m1}, dww(p + ".mlp.2"), 1, m2, true);

@@ -260,7 +260,9 @@ class Model {
             const View* aux = nullptr, const View* res = nullptr);
   ConvParams conv_params(const std::vector<View>& ins, const ConvW& w, int stride, int pad, const View& out, int epi,
                          const View* aux, const View* res);
-  void run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi = false);
+  void run_conv(const ConvParams& P, const ConvW& w, const _Float16* packed, bool hi = false, bool split = false);
+  void linatt_reproject(const View& k, const View& v, const View& q, int heads, int hd, int kmask, int qmask,
+                        const ConvW& rp, const View& a, const std::string& tag);
   void add_fusion_x4(const std::string& base, const float* w_dev, int Cout, hipStream_t st);
   void add_taps(const std::string& base, const float* w_dev, int Cin, hipStream_t st);
   bool taps_on() const;

@@ -187,6 +187,36 @@ def test_x4(shape):
     check(*run(X4, B, cin, cout, H, W, K, epi=epi))
 
 
+@pytest.mark.parametrize("shape", [
+    (2, 192, 768, 24, 64, 3, SHUFFLE | GELU),   # g_s subpel conv
+    (1, 192, 768, 19, 45, 3, SHUFFLE),          # ragged pixel tiles at every edge (clamped halo lines)
+    (1, 100, 200, 9, 33, 3, 0),                 # Cin not a multiple of 32
+    (2, 192, 192, 24, 40, 3, GELU),             # 192-row tile
+    (2, 256, 96, 17, 30, 5, 0),                 # 5x5, 96-row tile
+    (1, 288, 96, 13, 37, 5, 0),                 # 5x5, 128-row tile, few tiles: split-K on chunk bounds
+    (1, 480, 1920, 8, 16, 3, SHUFFLE | GELU),   # h_s subpel, few tiles: split-K
+])
+def test_x4_halo_vs_per_tap(shape):
+    """conv_x4's halo-staged B operand (one (8+K-1) x (32+K-1) image per 32-channel chunk, every tap a
+    shifted read of it) against B staged per tap: the same operands in the same MFMA order, so the
+    outputs are bit-identical whenever the K loop is not split; with split-K (few-tile shapes) the
+    halo form splits on chunk boundaries, so both are only checked against float64."""
+    from mlic_amd import _lib
+    B, cin, cout, H, W, K, epi = shape
+    try:
+        _lib.call("mlic_set_kernel_option", b"x4_halo", 1)
+        y1, ref = run(X4, B, cin, cout, H, W, K, epi=epi)
+        _lib.call("mlic_set_kernel_option", b"x4_halo", 0)
+        y0, _ = run(X4, B, cin, cout, H, W, K, epi=epi)
+    finally:
+        _lib.call("mlic_set_kernel_option", b"x4_halo", -1)
+    check(y1, ref)
+    check(y0, ref)
+    tiles = -(-cout // 256) * -(-W // 32) * -(-H // 8)
+    if tiles > 48:  # no split-K (conv_x4.hip x4_splitk)
+        assert torch.equal(y1, y0)
+
+
 def _conv_raw(impl, x, w, b, epi):
     from mlic_amd import _lib
     B, Cin, H, W = x.shape

@@ -643,6 +643,42 @@ def test_entropy_parameters_chain_vs_oracle(kind, idx, cin):
     assert err <= 2e-5 * max(1.0, float(exp.abs().max())), PARITY[f"chain_ep_{kind}{idx}"]
 
 
+@pytest.mark.parametrize("which,idx", [("inter", 3), ("inter", 9), ("intra", 1)])
+def test_linear_attention_fused_equals_unfused(golden, which, idx):
+    """The fused linear attention (one-launch ctx with its in-launch fixed-order combine, the output
+    written straight into the reprojection conv's packed operand) against the three-launch form with the
+    fp32 attention map: same arithmetic, bit-identical module outputs (context.py:140-245)."""
+    from mlic_amd import _lib
+    g = golden("modules_L.npz")
+    net = net_for("MLICPP_L")
+    T = lambda k: torch.from_numpy(g[k]).to(DEV)  # noqa: E731
+    a, b, o = {"inter": ("chan3_in" if idx == 3 else "inter9_in", None, "inter3_out" if idx == 3 else "inter9_out"),
+               "intra": ("intra_in1", "intra_in2", "intra_out")}[which]
+    outs = []
+    try:
+        for fused in (1, 0):
+            _lib.call("mlic_set_kernel_option", b"linatt_fused", fused)
+            outs.append(net.run_module(which, idx, T(a), None if b is None else T(b), out_shape=g[o].shape))
+            torch.cuda.synchronize()
+    finally:
+        _lib.call("mlic_set_kernel_option", b"linatt_fused", -1)
+    assert torch.equal(outs[0], outs[1])
+    # a batch of 3 with ragged splits through the fused path (1080p-latent-like width)
+    x = torch.randn(3, 32 * idx if which == "inter" else 32, 20, 36, generator=torch.Generator().manual_seed(idx)) * 2
+    x2 = torch.randn(3, 32, 20, 36, generator=torch.Generator().manual_seed(idx + 50)) * 2 if which == "intra" else None
+    outs = []
+    try:
+        for fused in (1, 0):
+            _lib.call("mlic_set_kernel_option", b"linatt_fused", fused)
+            shp = (3, 64, 20, 36)
+            outs.append(net.run_module(which, idx, x.to(DEV), None if x2 is None else x2.to(DEV), out_shape=shp))
+            torch.cuda.synchronize()
+    finally:
+        _lib.call("mlic_set_kernel_option", b"linatt_fused", -1)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_local_context_chain_ragged_vs_oracle():
     """LocalContext with its fused MLP chain at a ragged latent size, against the oracle."""
     net = net_for("MLICPP_L")
