@@ -94,7 +94,7 @@ def parse():
                          "default, else $MLIC_LANES or 4)")
     ap.add_argument("--precision", type=int, default=int(os.environ.get("MLIC_PRECISION", "2")),
                     help="dense-conv arithmetic: 2 = split-fp16 MFMA v2 + specialised kernels, "
-                         "1 = f16x3 v1 tiles, 0 = fp32 MFMA")
+                         "1 = f16x3 v1 tiles (A/B library only: make AB=1), 0 = fp32 MFMA")
     ap.add_argument("--synth-fp16", action="store_true",
                     help="SURVEY 8(f)4: g_s subpel convs on fp16 operands with fp32 accumulation (x_hat within "
                          "the 0.01 dB gate, bitstreams unchanged); default off: the headline stays fp32-faithful")

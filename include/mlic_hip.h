@@ -102,6 +102,10 @@ int mlic_set_poison(mlic_model* m, int on);
  * "linatt_fused" = the linear attention's one-launch context + its output written straight into the
  * reprojection conv's packed operand ($MLIC_LINATT_FUSED) */
 int mlic_set_kernel_option(const char* name, int value);
+/* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
+ * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the
+ * product build fails those requests loudly */
+int mlic_ab_families(int* built);
 /* fp16 range-guard fallbacks taken since the last reset (each changes the arithmetic of one call):
  * forward re-run whole in exact fp32 (the entropy model left fp16's range; compress refuses such an
  * input), forward's g_s alone, decompress's g_s alone (the same policy on both sides, so

@@ -47,6 +47,7 @@ def _sig(lib):
         "mlic_set_synthesis_precision": [p, i],
         "mlic_set_poison": [p, i],
         "mlic_set_kernel_option": [C.c_char_p, i],
+        "mlic_ab_families": [P(i)],
         "mlic_batch_stream": [p, i, i, p, sz, P(sz)],
         "mlic_decompress_batch_stream": [p, p, p, sz, P(p), P(sz), i, i, i, p, p],
         "mlic_range_fallbacks": [p, P(i64), P(i64), P(i64), i],
@@ -95,6 +96,13 @@ def poison() -> bool:
     Python layer NaN-fills the output tensors it hands to the library, so any element a kernel does
     not write, or any read of memory its producer never wrote, shows up as NaN."""
     return os.environ.get("MLIC_POISON", "0") not in ("", "0")
+
+
+def ab_families() -> bool:
+    """True when the loaded library holds the A/B-only kernel families (make AB=1)."""
+    v = C.c_int()
+    call("mlic_ab_families", C.byref(v))
+    return bool(v.value)
 
 
 def check(rc: int, what: str = ""):

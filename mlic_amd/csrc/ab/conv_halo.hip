@@ -17,8 +17,8 @@
 // context reprojection.  8 waves, each a 64(Cout) x (TH/4 rows x 32) sub-tile of
 // v_mfma_f32_32x32x16_f16 x 3 split terms.  Multi-segment (channel-concat) inputs are read in
 // place (segments are 16-channel aligned).  Epilogue = the shared conv_store.
-#include "common.h"
-#include "kernels.h"
+#include "../common.h"
+#include "../kernels.h"
 
 #include <cstdlib>
 

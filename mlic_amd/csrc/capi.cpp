@@ -217,6 +217,13 @@ int mlic_set_precision(mlic_model* m, int precision) {
   });
 }
 
+int mlic_ab_families(int* built) {
+  return guard([&] {
+    MLIC_CHECK(built, "null out");
+    *built = ab_families_built() ? 1 : 0;
+  });
+}
+
 int mlic_set_kernel_option(const char* name, int value) {
   return guard([&] {
     MLIC_CHECK(name, "null option name");

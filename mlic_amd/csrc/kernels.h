@@ -27,6 +27,9 @@ bool pw_resident_ok(const ConvParams& P, int cin_pad);
 void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 bool conv_narrow_ok(const ConvParams& P);
 void conv_narrow_forward(const ConvParams& P, hipStream_t st);
+// A/B-only families (ab/*.hip, make AB=1): v1 tiles, halo tiles, VALU local attention; the product
+// build links ab/ab_stubs.cpp instead (they throw; conv_halo_ok is false)
+bool ab_families_built();
 bool conv_halo_ok(const ConvParams& P, int cin_pad);
 void conv_halo_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 // g_s's N -> 12 3x3 output conv as 1x1 per-tap partials [B][108][H][W] + this gather (conv_pw.hip):
