@@ -816,8 +816,14 @@ constexpr bool x4_halo_fits() {
   constexpr int a = 2 * BM * ROWB, h = 2 * (TR + K - 1) * (TC + K - 1) * ROWB;
   return K > 1 && a + h <= 160 * 1024;
 }
+// Measured (tools/gpu/r4_halo.sh, 8 images, profiles/r04/ab/): 5x5 reprojection 320 -> 320 at 68 x 120
+// 1396 -> 1303 us; 3x3 g_s subpel conv 192 -> 768 at 272 x 480 7146 -> 7215 us and at 136 x 240 2133 ->
+// 2115 us (the per-tap fragment addresses become runtime: the swizzle of a tap-shifted line is
+// recomputed per read, which eats the saved B loads).  Default: 5x5 only; "x4_halo" = 1 forces it for
+// 3x3 too (A/B), 0 turns it off.
 static bool x4_halo(const ConvParams& P, bool hi) {
   if (!x4_halo_on() || P.K == 1 || P.stride != 1) return false;
+  if (P.K == 3 && g_x4_halo != 1) return false;
   const int bm = x4_bm(P.Cout);
   return 2 * bm * ROWB + 2 * (TR + P.K - 1) * (TC + P.K - 1) * ROWB <= 160 * 1024;
 }
