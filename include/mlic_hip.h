@@ -99,7 +99,7 @@ int mlic_set_synthesis_precision(mlic_model* m, int mode);
 int mlic_set_poison(mlic_model* m, int on);
 /* process-wide kernel A/B switches (tests, micro-benchmarks): "x4_halo" = the conv_x4 kernel's
  * halo-staged B operand for K x K stride-1 convs (1 on, 0 off, -1 default = $MLIC_X4_HALO or on);
- * "linatt_fused" = the linear attention's one-launch context + its output written straight into the
+ * "linatt_fused" = the linear attention's output written straight into the
  * reprojection conv's packed operand ($MLIC_LINATT_FUSED) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo

@@ -231,10 +231,7 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
   constexpr int QKP = LP_NCP * 16;       // halves per (tensor, head, hi|lo) plane
   constexpr int QK_H = 2 * 2 * 2 * QKP;  // q, k x heads x hi|lo
   constexpr int VP = 32 * LP_NCP;        // halves per v plane (hi or lo)
-  // staged output of one step (the 8 consecutive pixels the 8 waves compute): per query cell, the 8
-  // pixels' 128-byte lines (+16 bytes: the cells' rows fall on different banks), double-buffered
-  constexpr int OST = (8 * 128 + 16) / 2, OBUF = 25 * OST;  // halves
-  __shared__ __attribute__((aligned(16))) _Float16 sm[QK_H + 2 * VP + 2 * OBUF];
+  __shared__ __attribute__((aligned(16))) _Float16 sm[QK_H + 2 * VP];
   const int H = P.H, W = P.W, HW = H * W;
   const int b = blockIdx.y;
   const int ntx = (W + LP_TW - 1) / LP_TW;
@@ -314,14 +311,9 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
     }
   const int vrow = l32 & 15;
 
-  // step it: wave w computes pixel x0 + 8 it + w and stages its 25 lines; after the barrier the block
-  // stores, per query cell, the step's consecutive pixels as one contiguous run (full 128-byte lines;
-  // written from the lanes directly, each line would be assembled from 8-byte pieces of 8 stores)
-  for (int it = 0; it < LP_TW / LA_WAVES; ++it) {
-    const int lx = it * LA_WAVES + wave;
+  for (int lx = wave; lx < LP_TW; lx += LA_WAVES) {
     const int px = x0 + lx, py = y0;
-    _Float16* ost = sm + QK_H + 2 * VP + (it & 1) * OBUF;
-    if (px < W) {  // wave-uniform
+    if (px >= W) break;  // wave-uniform
     const int qcell = lvalid ? cy * LP_LW + lx + cx : LP_NCELL;
     const int par = (py + px) & 1;
     const bool interior = py >= 2 && py < H - 2 && px >= 2 && px < W - 2;  // wave-uniform
@@ -395,7 +387,7 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
     // O^T[d][i]: registers 0..3 are d = 4h .. 4h+3, registers 4..7 are d = 8 + 4h .. +3 of query i
     if (lvalid) {
       typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-      _Float16* dst = ost + l32 * OST + wave * 64;
+      _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + (int64_t)py * W + px) * 64;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
@@ -412,19 +404,6 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
           *reinterpret_cast<half4*>(dst + k) = hi;
           *reinterpret_cast<half4*>(dst + 32 + k) = lo;
         }
-    }
-    }  // px < W
-    // one barrier per step: the staged lines of every wave are visible; the buffer written two steps
-    // from now was last read before this barrier
-    __syncthreads();
-    const int nvalid = min(LA_WAVES, W - (x0 + it * LA_WAVES));  // pixels of this step inside the row
-    for (int cell = wave; cell < 25; cell += LA_WAVES) {
-      // the cell's run: nvalid lines = nvalid * 8 pieces of 16 bytes, one per lane
-      if (lane < nvalid * 8) {
-        const half8 v = *reinterpret_cast<const half8*>(ost + cell * OST + lane * 8);
-        *reinterpret_cast<half8*>(outp + (((int64_t)b * 25 + cell) * npos + (int64_t)y0 * W + x0 + it * LA_WAVES) * 64 +
-                                  lane * 8) = v;
-      }
     }
   }
 }

@@ -267,7 +267,10 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave + 8 * i) * 1024 + lane * 16) = ra[i];
     };
     // step s's MFMAs on LDS slot s & 1 (fragment reads one pixel group ahead)
-    auto mfma_step = [&](int s) {
+    // hook: the step's staging work (next slot's LDS stores, the loads two steps ahead), issued after
+    // the first pixel group's MFMAs, so that the step opens with its fragment reads and the LDS
+    // latency they expose overlaps the staging's register waits instead of following them
+    auto mfma_step = [&](int s, auto&& hook) {
       const char* As = sm + (s & 1) * A_BYTES;
       const char* Bs;
       int tapoff = 0;  // HALO: the tap's (ky, kx) shift in the halo image, in lines
@@ -317,6 +320,11 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           for (int i = 0; i < TM; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
         }
+        if (j == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          hook();
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     };
     if (HALO && s0 < s1) {  // the first chunk's halo image, whole
@@ -339,19 +347,26 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (s + 1 < s1) lstore(s + 1);
-      if constexpr (HALO) {
-        // the next chunk's halo: piece j - 1 stored and piece j loaded at local step j (the slot
-        // (cc + 1) & 1 was last read in chunk cc - 1, before this chunk's first barrier; its last
-        // piece lands at step NPH <= KK - 1, before chunk cc + 1's first barrier)
-        const int cc = s / KK, j = s - cc * KK;
-        if ((cc + 1) * KK < s1) {
-          if (j >= 1 && j <= NPH && hvalid(j - 1)) *reinterpret_cast<u32x4*>(hdst(j - 1, (cc + 1) & 1)) = hb;
-          if (j < NPH && hvalid(j)) hb = *reinterpret_cast<const u32x4*>(himg + (cc + 1) * plane + hsrc(j));
+      auto staging = [&]() __attribute__((always_inline)) {
+        if (s + 1 < s1) lstore(s + 1);
+        if constexpr (HALO) {
+          // the next chunk's halo: piece j - 1 stored and piece j loaded at local step j (the slot
+          // (cc + 1) & 1 was last read in chunk cc - 1, before this chunk's first barrier; its last
+          // piece lands at step NPH <= KK - 1, before chunk cc + 1's first barrier)
+          const int cc = s / KK, j = s - cc * KK;
+          if ((cc + 1) * KK < s1) {
+            if (j >= 1 && j <= NPH && hvalid(j - 1)) *reinterpret_cast<u32x4*>(hdst(j - 1, (cc + 1) & 1)) = hb;
+            if (j < NPH && hvalid(j)) hb = *reinterpret_cast<const u32x4*>(himg + (cc + 1) * plane + hsrc(j));
+          }
         }
+        if (s + 2 < s1) gload(s + 2);
+      };
+      if (abl & 16) {  // A/B: the round-3 order (staging first, then the step's reads and MFMAs)
+        staging();
+        mfma_step(s, [] {});
+      } else {
+        mfma_step(s, staging);
       }
-      if (s + 2 < s1) gload(s + 2);
-      mfma_step(s);
     }
     if constexpr (DIR) range_report(P.rflag, f16_unsafe(__uint_as_float(dmax)));
   } else {
@@ -845,7 +860,9 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
   const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
   dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B * nsplit);
   static const int abl = [] {
-    const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
+    // diagnostics: 1 = no DMA in the loop, 2 = no MFMA; A/B: 16 = register-staged steps in the round-3
+    // order (staging before the step's fragment reads)
+    const char* e = std::getenv("MLIC_X4_ABL");
     return e ? std::atoi(e) : 0;
   }();
   if (K == 1 && !act)

@@ -151,12 +151,11 @@ int64_t linear_attention_part_floats(int heads, int hd, int B, int nsplit);
 void linear_attention(const float* K, int64_t k_bs, const float* V, int64_t v_bs, const float* Q, int64_t q_bs,
                       float* out, int64_t o_bs, float* part, float* ctx, int heads, int hd, int H, int W, int B,
                       int nsplit, int kmask, int qmask, hipStream_t st);
-// the fused form: ctx = softmax_L(K) . V^T in ONE launch (partials + the last block's fixed-order
-// combine; cnt: B * heads counters, zeroed here), then linatt_pack (conv_x4.hip) computes
-// ctx^T . softmax_c(Q) straight into the packed operand of the conv that consumes the attention (P:
-// that conv's params; dst: x4_act_halves(P, P.Cin) halves)
+// the fused form: ctx = softmax_L(K) . V^T (partials + the fixed-order combine), then linatt_pack
+// (conv_x4.hip) computes ctx^T . softmax_c(Q) straight into the packed operand of the conv that
+// consumes the attention (P: that conv's params; dst: x4_act_halves(P, P.Cin) halves)
 void linear_attention_ctx(const float* K, int64_t k_bs, const float* V, int64_t v_bs, float* part, float* ctx,
-                          unsigned* cnt, int heads, int hd, int H, int W, int B, int nsplit, int kmask, hipStream_t st);
+                          int heads, int hd, int H, int W, int B, int nsplit, int kmask, hipStream_t st);
 void linatt_pack(const float* Q, int64_t q_bs, const float* ctx, int heads, int hd, int qmask, const ConvParams& P,
                  _Float16* dst, hipStream_t st);
 void ckbd_mask(const float* x, int64_t x_bs, float* y, int64_t y_bs, int C, int H, int W, int B, int keep_anchor,

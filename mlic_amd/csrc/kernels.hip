@@ -334,12 +334,11 @@ constexpr int CTX_CHUNK = 64;
 // record per (image, head, split): [HD] key maxima m_s, [HD][HD] sum_p exp(k_c - m_s) v_d,
 // [HD] sum_p exp(k_c - m_s).  256 threads; the K.V^T tile of thread t is a TC x TC block
 // (TC = HD / 16) read from pixel-major LDS copies as float2 pairs.
-// ctx_fused (cnt != null): the (image, head)'s last block to finish its record combines all nsplit records
-// in split order (ctx_reduce's arithmetic) into ctx -- one launch instead of two.  Hand-off per the
-// split-K recipe of cdna_hip_programming.md (Projection GEMM item 2): plain record stores, vmcnt(0),
-// barrier, agent-scope release fence, relaxed agent-scope ticket; the last arriver takes an agent-scope
-// acquire before reading the other blocks' records (correct wherever the blocks ran).  cnt[b * heads + h]
-// is zeroed by the host before the launch.
+// the fixed-order combine of one output's nsplit records (ctx_reduce_kernel).  Measured and rejected
+// (round 4): the combine inside the partial launch by each (image, head)'s last-arriving block
+// (agent-scope release fence + ticket per block, acquire in the last): 0.126 ms per inter-context call
+// at 8 x 68 x 120 against 0.105 for partial + this separate reduce + the old apply launch -- the release
+// fence of every one of the ~2200 blocks costs more than the launch it saves
 __device__ __forceinline__ void ctx_combine(const float* __restrict__ src, float* __restrict__ dst, int hd, int nsplit,
                                             int o) {
   const int nout = hd * hd, rec = hd * (hd + 2), c = o / hd;
@@ -359,8 +358,7 @@ template <int HD>
 __global__ __launch_bounds__(256) void ctx_partial_kernel(const float* __restrict__ K, int64_t k_bs,
                                                           const float* __restrict__ V, int64_t v_bs,
                                                           float* __restrict__ part, int heads, int H, int W,
-                                                          int nsplit, int kmask, float* __restrict__ ctx,
-                                                          unsigned* __restrict__ cnt) {
+                                                          int nsplit, int kmask) {
   constexpr int KP = HD + 2;                  // row pitch (floats): float2-aligned, 2-way write conflicts
   constexpr int NE = HD * CTX_CHUNK / 256;    // staged elements per thread per chunk: c = wave + 4 j, pixel = lane
   constexpr int TC = HD / 16;
@@ -443,24 +441,6 @@ __global__ __launch_bounds__(256) void ctx_partial_kernel(const float* __restric
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
     if (lane == 0) dst[HD + HD * HD + wave + 4 * j] = t;
   }
-  if (!cnt) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ int last;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(&cnt[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == (unsigned)(nsplit - 1) ? 1 : 0;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  const float* src = part + (int64_t)blockIdx.y * nsplit * (HD * (HD + 2));
-  for (int o = tid; o < HD * HD; o += 256) ctx_combine(src, ctx + (int64_t)blockIdx.y * HD * HD, HD, nsplit, o);
 }
 
 __global__ void ctx_reduce_kernel(const float* __restrict__ part, float* __restrict__ ctx, int hd, int nsplit,
@@ -517,15 +497,17 @@ int64_t linear_attention_part_floats(int heads, int hd, int B, int nsplit) {
 }
 
 void linear_attention_ctx(const float* K, int64_t k_bs, const float* V, int64_t v_bs, float* part, float* ctx,
-                          unsigned* cnt, int heads, int hd, int H, int W, int B, int nsplit, int kmask, hipStream_t st) {
+                          int heads, int hd, int H, int W, int B, int nsplit, int kmask, hipStream_t st) {
   MLIC_CHECK(hd == 16 || hd == 32, "head dim");
-  HIP_OK(hipMemsetAsync(cnt, 0, sizeof(unsigned) * B * heads, st));
   if (hd == 16)
     hipLaunchKernelGGL(ctx_partial_kernel<16>, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads,
-                       H, W, nsplit, kmask, ctx, cnt);
+                       H, W, nsplit, kmask);
   else
     hipLaunchKernelGGL(ctx_partial_kernel<32>, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads,
-                       H, W, nsplit, kmask, ctx, cnt);
+                       H, W, nsplit, kmask);
+  HIP_OK(hipGetLastError());
+  const int total = B * heads * hd * hd;
+  hipLaunchKernelGGL(ctx_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, ctx, hd, nsplit, total);
   HIP_OK(hipGetLastError());
 }
 
@@ -536,10 +518,10 @@ void linear_attention(const float* K, int64_t k_bs, const float* V, int64_t v_bs
   const int HW = H * W;
   if (hd == 16)
     hipLaunchKernelGGL(ctx_partial_kernel<16>, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads,
-                       H, W, nsplit, kmask, nullptr, nullptr);
+                       H, W, nsplit, kmask);
   else
     hipLaunchKernelGGL(ctx_partial_kernel<32>, dim3(nsplit, heads * B), dim3(256), 0, st, K, k_bs, V, v_bs, part, heads,
-                       H, W, nsplit, kmask, nullptr, nullptr);
+                       H, W, nsplit, kmask);
   HIP_OK(hipGetLastError());
   const int total = B * heads * hd * hd;
   hipLaunchKernelGGL(ctx_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, ctx, hd, nsplit, total);

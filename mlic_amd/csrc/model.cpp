@@ -1028,9 +1028,10 @@ static bool linatt_fused_on() {
 }
 
 // the linear attention and the 5x5 reprojection conv that consumes it (context.py:180-190, 235-241).
-// Fused (default, when the reprojection runs on conv_x4): ctx in one launch (partials + in-launch
-// combine), then ctx^T . softmax_c(q) written straight into the conv's packed split operand -- the
-// fp32 attention map is never stored.  Bit-identical to the unfused form (linatt_pack_kernel).
+// Fused (default, when the reprojection runs on conv_x4): ctx (partials + the fixed-order combine),
+// then ctx^T . softmax_c(q) written straight into the conv's packed split operand -- the fp32
+// attention map is never stored and the conv's own packing pass is gone.  Bit-identical to the
+// unfused form (linatt_pack_kernel).
 void Model::linatt_reproject(const View& k, const View& v, const View& q, int heads, int hd, int kmask, int qmask,
                              const ConvW& rp, const View& a, const std::string& tag) {
   const int H = q.H, W = q.W, HW = H * W, D = heads * hd, B = L().B;
@@ -1044,9 +1045,8 @@ void Model::linatt_reproject(const View& k, const View& v, const View& q, int he
   const ConvParams P = conv_params({geo}, rp, 1, 2, a, EPI_NONE, nullptr, nullptr);
   const ConvWeights cwt{rp.w, rp.wh, rp.wl, rp.cin_pad, rp.wx4, rp.wexp};
   if (linatt_fused_on() && rp.cin_pad == D && D % 32 == 0 && conv_select(P, cwt, prec()) == CONV_X4) {
-    unsigned* cnt = reinterpret_cast<unsigned*>(L().arena.alloc((int64_t)B * heads));
     timed(PCAT_LINATT, fl * 0.5, 4.0 * B * HW * D * 2.0, [&] {
-      linear_attention_ctx(k.p, k.bs, v.p, v.bs, part, ctx, cnt, heads, hd, H, W, B, nsplit, kmask, L().st);
+      linear_attention_ctx(k.p, k.bs, v.p, v.bs, part, ctx, heads, hd, H, W, B, nsplit, kmask, L().st);
     }, tag);
     _Float16* act = reinterpret_cast<_Float16*>(L().arena.alloc((2 * x4_act_halves(P, rp.cin_pad) + 3) / 4));
     timed(PCAT_LINATT, fl * 0.5, 4.0 * B * HW * D * 2.0, [&] {

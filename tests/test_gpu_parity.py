@@ -645,7 +645,7 @@ def test_entropy_parameters_chain_vs_oracle(kind, idx, cin):
 
 @pytest.mark.parametrize("which,idx", [("inter", 3), ("inter", 9), ("intra", 1)])
 def test_linear_attention_fused_equals_unfused(golden, which, idx):
-    """The fused linear attention (one-launch ctx with its in-launch fixed-order combine, the output
+    """The fused linear attention (ctx = partials + the fixed-order combine, the output
     written straight into the reprojection conv's packed operand) against the three-launch form with the
     fp32 attention map: same arithmetic, bit-identical module outputs (context.py:140-245)."""
     from mlic_amd import _lib
