@@ -361,12 +361,12 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
         }
         if (s + 2 < s1) gload(s + 2);
       };
-      if (abl & 16) {  // A/B: the round-3 order (staging first, then the step's reads and MFMAs)
-        staging();
-        mfma_step(s, [] {});
-      } else {
-        mfma_step(s, staging);
-      }
+#ifdef MLIC_X4_STAGING_FIRST  // A/B build: the round-3 order (staging, then the step's reads and MFMAs)
+      staging();
+      mfma_step(s, [] {});
+#else
+      mfma_step(s, staging);
+#endif
     }
     if constexpr (DIR) range_report(P.rflag, f16_unsafe(__uint_as_float(dmax)));
   } else {
@@ -860,9 +860,7 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
   const int ntx = (W + TC - 1) / TC, nty = (H + TR - 1) / TR;
   dim3 grid((P.Cout + BM - 1) / BM, ntx * nty, P.B * nsplit);
   static const int abl = [] {
-    // diagnostics: 1 = no DMA in the loop, 2 = no MFMA; A/B: 16 = register-staged steps in the round-3
-    // order (staging before the step's fragment reads)
-    const char* e = std::getenv("MLIC_X4_ABL");
+    const char* e = std::getenv("MLIC_X4_ABL");  // diagnostics: 1 = no DMA in the loop, 2 = no MFMA
     return e ? std::atoi(e) : 0;
   }();
   if (K == 1 && !act)
