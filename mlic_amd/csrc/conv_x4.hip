@@ -113,7 +113,21 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
     logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int ct = logical % nct, pt = logical / nct;
+  // tile order: Cout tiles fastest.  For GEMMs of many Cout tiles (the hoisted 640 -> 6400
+  // EntropyParameters hyper GEMM: 25 tiles of a 16 MB weight image) in groups of XG Cout tiles, the
+  // pixel tiles then advancing: the blocks an XCD runs back to back share XG weight slabs (2.6 MB,
+  // L2-resident) instead of cycling through the whole weight image per pixel tile
+  constexpr int XG = 4;
+  int ct, pt;
+  if (K == 1 && nct >= 2 * XG) {
+    const int band = XG * npt, g = logical / band, first = g * XG, r = logical - g * band;
+    const int gs = min(XG, nct - first);
+    ct = first + r % gs;
+    pt = r / gs;
+  } else {
+    ct = logical % nct;
+    pt = logical / nct;
+  }
   const int oy0 = (pt / ntx) * TR, ox0 = (pt % ntx) * TC;
   // split-K (nsplit > 1): blockIdx.z = image + B * split; the block runs steps [s0, s1) and stores
   // its raw partial sums into plane `split` of the partial buffer (P carries that layout, no epilogue)
