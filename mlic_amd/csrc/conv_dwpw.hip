@@ -295,7 +295,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
         const auto rs_out = dr_rsrc(P.out + (int64_t)b * P.out_bs, (uint32_t)P.Cout * cs4);
         const auto rs_res = dr_rsrc(RES ? P.res + (int64_t)b * P.res_bs : P.out, RES ? (uint32_t)P.Cout * cs4 : 0u);
         const float* sb = sbias + 4 * h;
-        const int wexp = P.wexp;
+        const float unscale = ldexpf(1.0f, -P.wexp);
         // checkerboard mask (MODE 4): keep a pixel where its anchor-ness matches the flag
         bool keep[2] = {true, true};
         if (MODE == 4 && (P.epi & (EPI_MASK_ANCHOR | EPI_MASK_NONANCHOR))) {
@@ -325,7 +325,10 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
           for (int q = 0; q < 16; ++q) {
             const float4 b4 = bq[q >> 2];
             const float bv = (q & 3) == 0 ? b4.x : (q & 3) == 1 ? b4.y : (q & 3) == 2 ? b4.z : b4.w;
-            float2v t = float2v{ldexpf(acc[c][0][q], -wexp), ldexpf(acc[c][1][q], -wexp)} + bv;
+            // acc * 2^-wexp + bias as one packed fma: the product by an exact power of two is exact (a
+            // subnormal result aside), so this equals ldexp then add (pw_resident does the same)
+            float2v t = __builtin_elementwise_fma(float2v{acc[c][0][q], acc[c][1][q]}, float2v{unscale, unscale},
+                                                  float2v{bv, bv});
             if constexpr (MODE == 1) t = gelu_erf2(t);
             if constexpr (MODE == 4) {
 #pragma unroll

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
     const uint32_t vo_aux = (uint32_t)p * 4u + (uint32_t)(4 * h) * ho4;
     const auto rs_res = make_rsrc(res ? P.res + (int64_t)b * P.res_bs : P.out, res ? (uint32_t)P.Cout * cs4 : 0u);
     const float* sb = sbias + 4 * h;  // per-lane base; the channel part folds into the ds_read offset
-    const int wexp = P.wexp;
+    const float unscale = ldexpf(1.0f, -P.wexp);
     // per co-tile: issue the 16 aux / residual loads together, then one wait, then 16 stores
     uint32_t so_o = 0, so_a = 0;  // channel byte offsets co_u * out_cs * 4 and co_u * HW * 4
     if (p < HW) {
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
         for (int r = 0; r < 16; ++r) {
           const float4 b4 = bq[r >> 2];
           const float bv = (r & 3) == 0 ? b4.x : (r & 3) == 1 ? b4.y : (r & 3) == 2 ? b4.z : b4.w;
-          float x = ldexpf(acc[c][r], -wexp) + bv;
+          float x = __builtin_fmaf(acc[c][r], unscale, bv);  // == ldexp(acc, -wexp) + bias (exact product)
           // fp16 range guard on the accumulator (an input beyond fp16 splits to inf/NaN and poisons it;
           // checked before GDN, whose rsqrt(inf) = 0 would hide it); cheaper here than in the ring
           bad |= !(fabsf(x) <= 3.4e38f);
