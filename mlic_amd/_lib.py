@@ -79,14 +79,32 @@ def _sig(lib):
     return lib
 
 
+def _check_build_record():
+    """The in-tree library must be the build of the sources in the tree (mlic_amd/build.py record)."""
+    import json
+    from . import build as _build
+    if os.environ.get("MLIC_HIP_LIB"):
+        return  # an explicitly chosen library (A/B builds): the caller vouches for it
+    rec_path = _build.RECORD
+    if not os.path.exists(rec_path):
+        raise MlicError(f"{rec_path} missing: rebuild with `python -m mlic_amd.build` (records the sources the "
+                        f"library was built from)")
+    with open(rec_path) as f:
+        rec = json.load(f)
+    if rec.get("sources_sha256") != _build.source_digest():
+        raise MlicError("libmlic_hip.so was built from other sources than the ones in this tree (stale build): "
+                        "rebuild with `python -m mlic_amd.build`")
+
+
 def lib():
-    """The loaded library (raises if it was not built)."""
+    """The loaded library (raises if it was not built, or was built from other sources)."""
     global _lib
     with _lock:
         if _lib is None:
             if not os.path.exists(LIB_PATH):
                 raise MlicError(f"libmlic_hip.so not found at {LIB_PATH}: build it with "
                                 f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            _check_build_record()
             _lib = _sig(C.CDLL(LIB_PATH))
     return _lib
 

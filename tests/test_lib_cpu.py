@@ -205,3 +205,15 @@ def test_file_bytes_is_the_written_file_size(vbr):
     buf.seek(0)
     hdr, strings, shape = bitstream.read_stream(buf, vbr=vbr)
     assert strings == [[y], [z]] and shape == (2, 4) and hdr[:2] == (120, 200)
+
+
+def test_build_record_matches_tree():
+    """The in-tree library carries a record of the sources it was built from (mlic_amd/build.py); it
+    matches the tree, and the recorded library digest is the library's."""
+    import hashlib
+    import json
+    from mlic_amd import build
+    rec = json.load(open(build.RECORD))
+    assert rec["sources_sha256"] == build.source_digest()
+    assert rec["library_sha256"] == hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    assert rec["target"] == "gfx950"
