@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--group-concurrency", type=int, default=0,
                     help="(weights, shape) batches of a step run concurrently, each on its own model "
                          "instance, lanes and stream (1 = one after another)")
+    ap.add_argument("--split", type=int, default=0,
+                    help="cut each (weights, shape) batch into this many request streams, each an independent "
+                         "compress -> decompress chain on its own model instance (0: the workload's default)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="run rank --emulate-rank's share of a W-rank job list on this one GPU, with 1/W of "
                          "the host cores (a prediction of one rank of a W-GPU run; value = that rank's img/s)")
@@ -120,6 +123,8 @@ def parse():
         a.lanes = int(os.environ["MLIC_LANES"]) if "MLIC_LANES" in os.environ else wl.get("lanes", 4)
     if a.group_concurrency <= 0:
         a.group_concurrency = wl.get("group_concurrency", 4)
+    if a.split <= 0:
+        a.split = wl.get("split", 1)
     return a
 
 
@@ -159,14 +164,16 @@ def build_jobs(a, rank: int, world: int):
     return jobs, per_rank * world
 
 
-def batches(jobs, max_pixels=32 * 1088 * 1920):
-    """Group jobs by (weights, shape) into batches of at most ~32 1080p images' worth of pixels."""
+def batches(jobs, max_pixels=32 * 1088 * 1920, split=1):
+    """Group jobs by (weights, shape) into batches of at most ~32 1080p images' worth of pixels, each
+    cut into `split` near-equal request streams."""
     out = {}
     for j in jobs:
         out.setdefault((j.model, j.rate, j.H, j.W), []).append(j)
     res = []
     for key, js in sorted(out.items(), key=lambda kv: (str(kv[0][1]), kv[0][2], kv[0][3])):
         cap = max(1, max_pixels // (key[2] * key[3]))
+        cap = min(cap, -(-len(js) // max(1, split)))
         for i in range(0, len(js), cap):
             res.append((key, js[i:i + cap]))
     return res
@@ -267,7 +274,7 @@ def main():
     from mlic_amd import dist as mdist
     wl = WORKLOADS[a.config]
     jobs, n_jobs_total = build_jobs(a, jrank, jworld)
-    groups = batches(jobs)
+    groups = batches(jobs, split=a.split)
     # biggest batches first: the concurrent groups finish together
     order = sorted(range(len(groups)), key=lambda gi: -len(groups[gi][1]) * groups[gi][0][2] * groups[gi][0][3])
     conc = max(1, min(a.group_concurrency, len(groups)))

@@ -143,10 +143,9 @@ int mlic_encoded_streams(mlic_model* m, int b, int64_t* n_y, int64_t* n_z, int32
                          int32_t* z_sym) {
   return guard([&] {
     const EncodedImage& e = impl(m).encoded(b);
-    *n_y = (int64_t)e.y_sym.size();
+    *n_y = e.y_in.size();
     *n_z = (int64_t)e.z_sym.size();
-    if (y_sym) std::memcpy(y_sym, e.y_sym.data(), e.y_sym.size() * 4);
-    if (y_idx) std::memcpy(y_idx, e.y_idx.data(), e.y_idx.size() * 4);
+    e.y_in.gather(y_sym, y_idx);
     if (z_sym) std::memcpy(z_sym, e.z_sym.data(), e.z_sym.size() * 4);
   });
 }

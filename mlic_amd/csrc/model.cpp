@@ -462,6 +462,10 @@ Lane::~Lane() {
   if (rflag) (void)hipFree(rflag);
   if (h_sym) (void)hipHostFree(h_sym);
   if (h_idx) (void)hipHostFree(h_idx);
+  if (hc_sym) (void)hipHostFree(hc_sym);
+  if (hc_idx) (void)hipHostFree(hc_idx);
+  if (cev) (void)hipEventDestroy(cev);
+  if (cst) (void)hipStreamDestroy(cst);
   for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
   if (own_stream && st) (void)hipStreamDestroy(st);
 }
@@ -1271,6 +1275,14 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.idx = d_idx + (int64_t)phase_id * L().B * n_per;
         }
         timed(PCAT_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); }, "quant_phase");
+        Lane& l = L();
+        if (mode == Mode::Encode && l.phase_d2h && !l.dry) {  // this phase's coder inputs leave now
+          const int64_t off = (int64_t)phase_id * l.B * n_per, nb = sizeof(int32_t) * l.B * n_per;
+          HIP_OK(hipEventRecord(l.cev, l.st));
+          HIP_OK(hipStreamWaitEvent(l.cst, l.cev, 0));
+          HIP_OK(hipMemcpyAsync(l.hc_sym + off, Q.sym, nb, hipMemcpyDeviceToHost, l.cst));
+          HIP_OK(hipMemcpyAsync(l.hc_idx + off, Q.idx, nb, hipMemcpyDeviceToHost, l.cst));
+        }
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
       lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
@@ -1328,6 +1340,21 @@ void Model::ensure_host(size_t n) {
   HIP_OK(hipHostMalloc(&l.h_sym, n * sizeof(int32_t)));
   HIP_OK(hipHostMalloc(&l.h_idx, n * sizeof(int32_t)));
   l.h_cap = n;
+}
+
+void Model::ensure_chost(size_t n) {
+  Lane& l = L();
+  if (!l.cst) {
+    HIP_OK(hipStreamCreateWithFlags(&l.cst, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&l.cev, hipEventDisableTiming));
+  }
+  if (n <= l.hc_cap) return;
+  if (l.hc_sym) HIP_OK(hipHostFree(l.hc_sym));
+  if (l.hc_idx) HIP_OK(hipHostFree(l.hc_idx));
+  l.hc_sym = l.hc_idx = nullptr;
+  HIP_OK(hipHostMalloc(&l.hc_sym, n * sizeof(int32_t)));
+  HIP_OK(hipHostMalloc(&l.hc_idx, n * sizeof(int32_t)));
+  l.hc_cap = n;
 }
 
 void Model::set_vbr(const float* scales, int B) {
@@ -1585,6 +1612,12 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   int32_t *d_sym = nullptr, *d_idx = nullptr, *d_zsym = nullptr;
   double* d_bits = nullptr;  // [2][B]: -log2 likelihood sums of y and z per image (B1, rd_loss.py:42-45)
   range_clear(l);
+  ensure_chost((size_t)(ny + nz));
+  l.phase_d2h = true;
+  struct Off {
+    Lane& l;
+    ~Off() { l.phase_d2h = false; }
+  } phase_off{l};
   planned(B, nullptr, [&] {
     d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
     d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
@@ -1601,7 +1634,7 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     eb(z, zh, z_lik, d_zsym);  // z_hat = round(z - med) + med == decompress(compress(z))
     View hyper = h_s(zh);
     View yhat = alloc(cfg_.M, y.H, y.W);
-    slice_loop(Mode::Encode, hyper, &y, yhat, y_lik, d_sym, d_idx, nullptr);
+    slice_loop(Mode::Encode, hyper, &y, yhat, y_lik, d_sym, d_idx, nullptr);  // phases leave on l.cst
     timed(PCAT_ELEM, 0.0, 4.0 * B * (ny_img + nz_img), [&] {
       neglog2_sum(y_lik, ny_img, B, d_bits, part, l.st);
       neglog2_sum(z_lik, nz_img, B, d_bits + B, part + neglog2_partial_doubles(B), l.st);
@@ -1609,16 +1642,14 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   });
   std::vector<double> bits(2 * B);
   HIP_OK(hipMemcpyAsync(bits.data(), d_bits, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, l.st));
-  ensure_host((size_t)(ny + nz));
-  int32_t* hs = l.h_sym;
-  int32_t* hi = l.h_idx;
-  int32_t* hzs = l.h_sym + ny;
-  HIP_OK(hipMemcpyAsync(hs, d_sym, ny * 4, hipMemcpyDeviceToHost, l.st));
-  HIP_OK(hipMemcpyAsync(hi, d_idx, ny * 4, hipMemcpyDeviceToHost, l.st));
+  const int32_t* hs = l.hc_sym;
+  const int32_t* hi = l.hc_idx;
+  int32_t* hzs = l.hc_sym + ny;
   HIP_OK(hipMemcpyAsync(hzs, d_zsym, nz * 4, hipMemcpyDeviceToHost, l.st));
   {
     HostStats::Scope w{hstats_.wait_ns};
     HIP_OK(hipStreamSynchronize(l.st));
+    HIP_OK(hipStreamSynchronize(l.cst));
   }
   if (prec() != PREC_F32 && range_hit(l)) throw Error(kRangeMsg);
   l.enc.assign(B, EncodedImage{});
@@ -1629,15 +1660,13 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   const int64_t zper = (int64_t)cfg_.N * hz * wz;
   auto work = [&](int b) {
     HostStats::Scope e{hstats_.enc_ns};
-    // y: phases in order, this image's part of each ([phase][B][n_per] on device)
-    std::vector<int32_t> s((size_t)nph * n_per), ix((size_t)nph * n_per);
-    for (int k = 0; k < nph; ++k) {
-      std::memcpy(s.data() + k * n_per, hs + ((int64_t)k * B + b) * n_per, n_per * 4);
-      std::memcpy(ix.data() + k * n_per, hi + ((int64_t)k * B + b) * n_per, n_per * 4);
-    }
-    l.enc[b].y = rans_encode(s.data(), ix.data(), (int64_t)s.size(), gc_);
-    l.enc[b].y_sym = std::move(s);
-    l.enc[b].y_idx = std::move(ix);
+    // y: phases in order, this image's part of each ([phase][B][n_per] in the pinned buffers), coded
+    // straight from there: rANS codes LIFO, so the last phase goes in first
+    CoderView v{hs + b * n_per, hi + b * n_per, n_per, (int64_t)B * n_per, nph};
+    RansEncoder enc(v.size());
+    for (int k = nph; k-- > 0;) enc.put_reverse(v.sym + k * v.stride, v.idx + k * v.stride, n_per, gc_);
+    l.enc[b].y = enc.flush();
+    l.enc[b].y_in = v;
     l.enc[b].z_sym.assign(hzs + b * zper, hzs + (b + 1) * zper);
     // z: EntropyBottleneck._build_indexes -> channel index, C-order over [C, hz, wz]
     std::vector<int32_t> zi(zper);
@@ -1674,19 +1703,18 @@ void Model::decompress(const uint8_t* const* y, const size_t* ylen, const uint8_
 
 std::string Model::batch_stream(int first, int count) const {
   MLIC_CHECK(first >= 0 && count >= 1 && first + count <= (int)enc_all_.size(), "batch_stream: image range");
-  const size_t n = enc_all_[first].y_sym.size();
-  const int64_t n_per = (int64_t)n / (2 * cfg_.S);
-  std::vector<int32_t> s, ix;
-  s.reserve(n * count);
-  ix.reserve(n * count);
-  for (int k = 0; k < 2 * cfg_.S; ++k)
-    for (int b = first; b < first + count; ++b) {
-      const EncodedImage& e = enc_all_[b];
-      MLIC_CHECK(e.y_sym.size() == n, "batch_stream: images of one shape");
-      s.insert(s.end(), e.y_sym.begin() + k * n_per, e.y_sym.begin() + (k + 1) * n_per);
-      ix.insert(ix.end(), e.y_idx.begin() + k * n_per, e.y_idx.begin() + (k + 1) * n_per);
+  const CoderView& v0 = enc_all_[first].y_in;
+  const int64_t n_per = v0.n_per;
+  for (int b = first; b < first + count; ++b)
+    MLIC_CHECK(enc_all_[b].y_in.n_per == n_per && enc_all_[b].y_in.nph == v0.nph, "batch_stream: images of one shape");
+  // phase-major, image-minor: coded LIFO, so the last phase's last image goes in first
+  RansEncoder enc(v0.size() * count);
+  for (int k = v0.nph; k-- > 0;)
+    for (int b = first + count; b-- > first;) {
+      const CoderView& v = enc_all_[b].y_in;
+      enc.put_reverse(v.sym + k * v.stride, v.idx + k * v.stride, n_per, gc_);
     }
-  return rans_encode(s.data(), ix.data(), (int64_t)s.size(), gc_);
+  return enc.flush();
 }
 
 // mlicpp.py:292-378 for the lane's images: z decoded on the host, then 20 phases of
@@ -1701,11 +1729,12 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
   {
     std::vector<int32_t> zi(zper);
     for (int64_t i = 0; i < zper; ++i) zi[i] = (int32_t)(i / ((int64_t)hz * wz));
-    for (int b = 0; b < B; ++b) {
-      RansDecoderState d;
-      d.set_stream(z[b], zlen[b]);
-      d.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
-    }
+    host_pool().run(B, [&](int b) {  // one z stream per image, decoded in parallel
+      HostStats::Scope d{hstats_.dec_ns};
+      RansDecoderState dz;
+      dz.set_stream(z[b], zlen[b]);
+      dz.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
+    });
   }
   PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool(), batch_stream);
   const int32_t* hz_sym = l.h_sym;

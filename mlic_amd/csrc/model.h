@@ -5,6 +5,7 @@
 #include <chrono>
 #include <map>
 #include <memory>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -87,10 +88,27 @@ struct ProfStat {
   double ms = 0, flops = 0, bytes = 0;
 };
 
+// An image's y coder inputs where compress left them: the lane's pinned phase-major buffers
+// ([phase][B][n_per]), valid until the model's next compress()
+struct CoderView {
+  const int32_t* sym = nullptr;
+  const int32_t* idx = nullptr;
+  int64_t n_per = 0, stride = 0;  // symbols per phase of one image; distance between phases
+  int nph = 0;
+  int64_t size() const { return n_per * nph; }
+  void gather(int32_t* s, int32_t* i) const {  // coder order: phases in order
+    for (int k = 0; k < nph; ++k) {
+      if (s) std::memcpy(s + k * n_per, sym + k * stride, n_per * 4);
+      if (i) std::memcpy(i + k * n_per, idx + k * stride, n_per * 4);
+    }
+  }
+};
+
 struct EncodedImage {
   std::string y;  // one rANS stream for all slices/phases
   std::string z;  // z stream (EntropyBottleneck)
-  std::vector<int32_t> y_sym, y_idx, z_sym;  // the coder inputs, in coder order (tests / tooling)
+  CoderView y_in;              // the y coder inputs (tests / tooling / batch_stream)
+  std::vector<int32_t> z_sym;  // the z coder inputs
   double y_bits = 0, z_bits = 0;  // sum of -log2 of the y / z likelihoods (rd_loss.py:42-45 numerator)
 };
 
@@ -123,6 +141,14 @@ struct Lane {
   int32_t* h_sym = nullptr;
   int32_t* h_idx = nullptr;
   size_t h_cap = 0;
+  // compress: every phase's symbols / indexes leave for these pinned buffers on the copy stream as
+  // soon as the phase is quantised, so only the last phase's copy is left when the network ends
+  hipStream_t cst = nullptr;
+  hipEvent_t cev = nullptr;
+  int32_t* hc_sym = nullptr;
+  int32_t* hc_idx = nullptr;
+  size_t hc_cap = 0;
+  bool phase_d2h = false;
   // profiling
   struct ProfRec {
     hipEvent_t a, b;
@@ -297,6 +323,7 @@ class Model {
   template <class F>
   void planned(int B, hipStream_t st, F&& body);
   void ensure_host(size_t n);
+  void ensure_chost(size_t n);
   void set_vbr(const float* scales, int B);
 };
 

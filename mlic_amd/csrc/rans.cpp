@@ -50,7 +50,7 @@ EncSym make_enc_sym(uint32_t start, uint32_t freq) {
 
 inline void enc_put_sym(uint64_t& x, uint32_t*& ptr, const EncSym& s) {
   const uint64_t x_max = ((RANS64_L >> PRECISION) << 32) * s.freq;
-  if (x >= x_max) {
+  if (x >= x_max) {  // rare on low-entropy streams: a predictable branch beats a select on the state's path
     *--ptr = (uint32_t)x;
     x >>= 32;
   }
@@ -69,34 +69,44 @@ inline void enc_put_bits(uint64_t& x, uint32_t*& ptr, uint32_t val, uint32_t nbi
 }
 }  // namespace
 
-std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t) {
+RansEncoder::RansEncoder(int64_t n_hint) : out_((size_t)std::max<int64_t>(n_hint, 0) + 64, 0u) {
+  end_ = out_.data() + out_.size();
+  ptr_ = end_;
+}
+
+void RansEncoder::grow() {  // keep the written tail at the end of a larger buffer
+  const size_t used = (size_t)(end_ - ptr_);
+  std::vector<uint32_t> bigger(out_.size() * 2 + 64, 0u);
+  std::memcpy(bigger.data() + bigger.size() - used, ptr_, used * 4);
+  out_.swap(bigger);
+  end_ = out_.data() + out_.size();
+  ptr_ = end_ - used;
+}
+
+void RansEncoder::put_reverse(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t) {
   if (t.enc.empty()) throw std::runtime_error("rans: tables not prepared");
   // One reverse pass.  compressai pushes, per symbol: the symbol (value clamped to max_value) and,
   // if escaped, the bypass length nb (< 15 for 32-bit values) and nb 4-bit chunks of the raw
   // value; the coder consumes that stream LIFO, so walking symbols backwards we emit the raw
   // chunks (last first), then nb, then the symbol.  Each emit writes at most one 32-bit word.
-  std::vector<uint32_t> out((size_t)n + 64, 0u);
-  uint32_t* end = out.data() + out.size();
-  uint32_t* ptr = end;
-  uint64_t x = RANS64_L;
+  uint32_t* ptr = ptr_;
+  uint64_t x = x_;
   const EncSym* es = t.enc.data();
   const int32_t* len = t.length.data();
   const int32_t* off = t.offset.data();
   const int stride = t.stride;
+  const uint32_t ntab = (uint32_t)t.n;
   for (int64_t i = n; i-- > 0;) {
-    if ((size_t)(ptr - out.data()) < 16) {  // grow: keep the written tail at the end of a larger buffer
-      const size_t used = (size_t)(end - ptr);
-      std::vector<uint32_t> bigger(out.size() * 2 + 64, 0u);
-      std::memcpy(bigger.data() + bigger.size() - used, ptr, used * 4);
-      out.swap(bigger);
-      end = out.data() + out.size();
-      ptr = end - used;
+    if ((size_t)(ptr - out_.data()) < 16) {
+      ptr_ = ptr;
+      grow();
+      ptr = ptr_;
     }
     const int32_t ci = indexes[i];
-    if ((uint32_t)ci >= (uint32_t)t.n) throw std::runtime_error("rans: cdf index out of range");
+    if ((uint32_t)ci >= ntab) throw std::runtime_error("rans: cdf index out of range");
     const int32_t max_value = len[ci] - 2;
     int32_t value = symbols[i] - off[ci];
-    if (value < 0 || value >= max_value) {
+    if ((uint32_t)value >= (uint32_t)max_value) {  // value < 0 or value >= max_value
       const uint32_t raw = value < 0 ? (uint32_t)(-2 * (int64_t)value - 1) : (uint32_t)(2 * ((int64_t)value - max_value));
       int32_t nb = 0;
       while (nb < 8 && (raw >> (nb * BYPASS_PRECISION)) != 0) ++nb;
@@ -106,11 +116,23 @@ std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t 
     }
     enc_put_sym(x, ptr, es[(int64_t)ci * stride + value]);
   }
-  ptr -= 2;  // flush
-  ptr[0] = (uint32_t)(x >> 0);
-  ptr[1] = (uint32_t)(x >> 32);
-  const size_t nbytes = (size_t)(end - ptr) * sizeof(uint32_t);
-  return std::string(reinterpret_cast<const char*>(ptr), nbytes);
+  ptr_ = ptr;
+  x_ = x;
+}
+
+std::string RansEncoder::flush() {
+  if ((size_t)(ptr_ - out_.data()) < 2) grow();
+  ptr_ -= 2;
+  ptr_[0] = (uint32_t)(x_ >> 0);
+  ptr_[1] = (uint32_t)(x_ >> 32);
+  const size_t nbytes = (size_t)(end_ - ptr_) * sizeof(uint32_t);
+  return std::string(reinterpret_cast<const char*>(ptr_), nbytes);
+}
+
+std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t) {
+  RansEncoder e(n);
+  e.put_reverse(symbols, indexes, n, t);
+  return e.flush();
 }
 
 void RansDecoderState::set_stream(const uint8_t* data, size_t nbytes) {

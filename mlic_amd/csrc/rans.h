@@ -33,6 +33,24 @@ struct CdfTables {
 // Encodes symbols[i] with table indexes[i]; returns the byte string (little-endian u32 words).
 std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t);
 
+// The same coder over a stream given in pieces: rANS codes LIFO, so the pieces are handed over
+// last first (put_reverse(piece k) for k = last .. 0), each walked backwards; flush() then returns
+// exactly rans_encode() of the concatenation.  Lets the caller code an image's phases straight from
+// the phase-major batch buffers without gathering them.
+class RansEncoder {
+ public:
+  explicit RansEncoder(int64_t n_hint);
+  void put_reverse(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t);
+  std::string flush();
+
+ private:
+  std::vector<uint32_t> out_;
+  uint32_t* end_;
+  uint32_t* ptr_;
+  uint64_t x_ = 1ull << 31;  // RANS64_L
+  void grow();
+};
+
 class RansDecoderState {
  public:
   void set_stream(const uint8_t* data, size_t nbytes);
