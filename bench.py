@@ -62,7 +62,10 @@ def family(cat_name: str) -> str:
 
 
 WORKLOADS = {
-    "main": dict(model="MLICPP_L", groups=[(1088, 1920, 32)], scaling="weak",
+    # the 32 images of a step as 4 request streams of 8 (2 lanes each): a stream's decompress starts as
+    # soon as its own compress + rANS encode is done, instead of every lane waiting for the slowest
+    # lane's encode (measured 86.9-88.1 img/s against 83.0-85.7 as one 32-image call on 4 lanes)
+    "main": dict(model="MLICPP_L", groups=[(1088, 1920, 32)], scaling="weak", split=4, lanes=2,
                  desc="config 2: MLICPP_L compress+decompress of 1920x1088 images"),
     "kodak": dict(model="MLICPP_L", groups=[(512, 768, 64)], scaling="weak",
                   desc="config 1 shape on GPU: MLICPP_L compress+decompress of 768x512 (Kodak-size) images"),
@@ -443,6 +446,7 @@ def main():
                        "weights": ("high-rate set (round 1)" if cfg0[1] is None else
                                    f"rate set(s) {sorted({k[1] for k, _ in groups})} of synthetic.RATE_LAMBDAS"),
                        "parallelism": f"image-sharded x{world} (no cross-GPU context)",
+                       "request_streams": len(groups), "lanes_per_stream": a.lanes,
                        **({"synthesis": "fp16 operands (SURVEY f4)"} if a.synth_fp16 else {})},
             "roofline": roofline,
             **prof,
@@ -534,7 +538,9 @@ def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev):
 
     prof_lanes = a.profile_lanes or a.lanes
     fam, _ = profile_pass(prof_lanes)
-    share = max(1, groups[0][1].__len__() // prof_lanes)
+    # isolated pass: one lane on 8 images of the first batch (the r04 records' unit: bench.py --lanes 1
+    # --batch 8 --split 1 under rocprofv3 profiles the same launches)
+    share = min(8, len(groups[0][1]))
     fam1, layer_rows1 = profile_pass(1, share)
     if a.layers_out and int(os.environ.get("RANK", "0")) == 0:
         with open(a.layers_out, "w") as f:  # isolated launches: the per-layer efficiency table
@@ -553,7 +559,7 @@ def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev):
 
     # The headline roofline is the kernel's own: launch durations of the isolated pass (one lane running
     # one lane's share of the first batch, each launch alone on the GPU -- reproducible with
-    # `rocprofv3 --kernel-trace --stats -- python bench.py --lanes 1 --batch <share>`).  The timed
+    # `rocprofv3 --kernel-trace --stats -- python bench.py --lanes 1 --batch 8 --split 1`).  The timed
     # configuration's launches overlap across lanes, so their HIP-event durations include other lanes'
     # kernels; they are kept as the secondary `concurrent` entry.
     # dominant = the family with the most isolated device time

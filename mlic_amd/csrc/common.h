@@ -166,16 +166,17 @@ __device__ __forceinline__ mlic_float2 gelu_erf2(mlic_float2 x) {
   const mlic_float2 m = {__builtin_fmaxf(x.x, 0.0f), __builtin_fmaxf(x.y, 0.0f)};
   return m - ax * (q * e);
 }
-// the conv / depthwise epilogues' GELU: torch's own formula 0.5 x (1 + erf(x / sqrt 2)) on the
-// library erff.  Its branches keep those epilogues' fully unrolled element loops small (the
-// branch-free gelu_erf, evaluated for every element there, pushes them past the unroller's budget or
-// up in registers); gelu_erf serves the chain kernel, where it is interleaved with MFMAs, and the
-// pw_resident / dwpw epilogues, whose element loops are short
+// torch's own formula 0.5 x (1 + erf(x / sqrt 2)) on the library erff: the x3v2 tiles' epilogue, whose
+// fully unrolled element loops the branch-free form pushes into scratch (576 B per lane)
+__device__ __forceinline__ float gelu_erff(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+// every other conv / depthwise epilogue's GELU (x4, pw_resident, dwpw, the exact-fp32 MFMA convs, the
+// depthwise kernels): the chain kernel's branch-free gelu_erf (round 4: the g_s subpel convs' GELU
+// epilogue 0.7 -> 0.3 ms of 7.7 per 8 images; library erff spends ~25 VALU per value on its branches)
 __device__ __forceinline__ float gelu_epi(float x) {
-#ifdef MLIC_GELU_EPI_FAST  // A/B build only: the chain kernel's branch-free form in the conv epilogues
+#ifndef MLIC_GELU_EPI_ERFF  // A/B build: -DMLIC_GELU_EPI_ERFF = the library form everywhere
   return gelu_erf(x);
 #else
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  return gelu_erff(x);
 #endif
 }
 

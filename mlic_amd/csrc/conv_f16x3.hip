@@ -266,7 +266,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_x3v2_kernel(ConvP
         float v = acc[i][j][r];
         v = ldexpf(v, -P.wexp);
         if (P.bias) v += P.bias[co];
-        if (epi & EPI_GELU) v = gelu_epi(v);
+        if (epi & EPI_GELU) v = gelu_erff(v);
         if (epi & (EPI_GDN | EPI_IGDN)) {
           const float x = P.aux[(int64_t)b * P.aux_bs + (int64_t)co * HWo + p];
           v = (epi & EPI_GDN) ? x * (1.0f / sqrtf(v)) : x * sqrtf(v);

@@ -3,7 +3,7 @@
 # stages (default "tests pmc bench rocprof"):
 #   tests    GPU suite (workspace + outputs NaN-poisoned, tests/conftest.py) with exact parity counts
 #   pmc      FETCH_SIZE / WRITE_SIZE of the dominant family over the isolated pass's launches
-#            (one lane, 8 images: bench.py --lanes 1 --batch 8), tools/pmc_traffic.py -> traffic.json
+#            (one lane, 8 images: bench.py --lanes 1 --batch 8 --split 1), tools/pmc_traffic.py -> traffic.json
 #   bench    the default bench line (roofline.traffic from traffic.json) + per-layer table
 #   rocprof  rocprofv3 --kernel-trace --stats of the isolated pass alone (the launches the line's
 #            roofline.frac divides by) and of the timed configuration alone
@@ -11,7 +11,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/record}
 KERN=${2:-conv_x4_kernel}
 STAGES=${3:-"tests pmc bench rocprof"}
-ISO="--lanes 1 --batch 8"
+ISO="--lanes 1 --batch 8 --split 1"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
@@ -33,7 +33,7 @@ if has pmc; then
     python3 -u bench.py $ISO --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > "$OUT/pmc_write.log" 2>&1 ||
     { echo "pmc write failed $?"; tail -20 "$OUT/pmc_write.log"; exit 1; }
   python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$KERN" "$OUT/traffic.json" config=main \
-    "launches_of=isolated pass: bench.py --lanes 1 --batch 8 --steps 1 --warmup 0 (the launches roofline.frac divides by)" || exit 1
+    "launches_of=isolated pass: bench.py --lanes 1 --batch 8 --split 1 --steps 1 --warmup 0 (the launches roofline.frac divides by)" || exit 1
   rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write"
 fi
 if has bench; then
