@@ -100,7 +100,8 @@ int mlic_set_poison(mlic_model* m, int on);
 /* process-wide kernel A/B switches (tests, micro-benchmarks): "x4_halo" = the conv_x4 kernel's
  * halo-staged B operand for K x K stride-1 convs (1 on, 0 off, -1 default = $MLIC_X4_HALO or on);
  * "linatt_fused" = the linear attention's output written straight into the
- * reprojection conv's packed operand ($MLIC_LINATT_FUSED) */
+ * reprojection conv's packed operand ($MLIC_LINATT_FUSED); "dw_strip" = the register-strip depthwise
+ * 3x3 for stride-1 planes up to 64 columns ($MLIC_DW_STRIP) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
  * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the

@@ -229,6 +229,7 @@ int mlic_set_kernel_option(const char* name, int value) {
     const std::string n = name;
     if (n == "x4_halo") x4_set_halo(value);
     else if (n == "linatt_fused") linatt_set_fused(value);
+    else if (n == "dw_strip") dw_set_strip(value);
     else throw Error("mlic: unknown kernel option " + n);
   });
 }

@@ -254,8 +254,12 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
                         float unscale) {
     const int j = pi >> 2, q = (pi >> 1) & 1, e = 2 * (pi & 1);
     const float* bq = sbias + boff + 32 * c + 16 * q + 4 * G + e;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) v[j][4 * q + e + k] = gelu_erf(__builtin_fmaf(acc[2 * c + q][j][e + k], unscale, bq[k]));
+    // the pair through the packed GELU (gelu_erf2 == gelu_erf element for element) and one packed fma
+    const mlic_float2 a2 = __builtin_elementwise_fma(mlic_float2{acc[2 * c + q][j][e], acc[2 * c + q][j][e + 1]},
+                                                     mlic_float2{unscale, unscale}, mlic_float2{bq[0], bq[1]});
+    const mlic_float2 g2 = gelu_erf2(a2);
+    v[j][4 * q + e] = g2.x;
+    v[j][4 * q + e + 1] = g2.y;
     if ((pi & 3) == 3) split8(v[j], oh[j], ol[j]);
   };
 

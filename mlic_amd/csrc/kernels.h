@@ -124,6 +124,7 @@ struct DwParams {
   int B;
 };
 void dw3x3(const DwParams& P, hipStream_t st);
+void dw_set_strip(int v);  // A/B: 0 = the LDS-tile kernel for narrow stride-1 planes too
 
 void ln_channels(const float* x, int64_t x_bs, float* y, int64_t y_bs, const float* g, const float* b, int C,
                  int HW, int B, hipStream_t st);

@@ -349,6 +349,41 @@ def test_depthwise(shape):
     check(y, ref.float(), rtol=1e-6)
 
 
+@pytest.mark.parametrize("B,Cn,H,W,gelu", [
+    (2, 224, 32, 48, 0),    # Kodak-size latent: 12 float4 columns, 5 strips per wave, R = 17 (2 strips)
+    (3, 64, 32, 48, 1),     # GELU
+    (1, 32, 68, 64, 1),     # 16 columns: 4 strips per wave; 68 rows = 4 x 17
+    (2, 96, 9, 16, 0),      # 4 columns, 16 strips per wave; R = 8 / 12 tails
+    (1, 40, 1, 8, 1),       # a single row: both vertical taps out of the image
+    (2, 128, 25, 60, 0),    # 15 columns: the last lane pair of each strip at the wave seam
+])
+def test_depthwise_strip_vs_tile(B, Cn, H, W, gelu):
+    """The register-strip depthwise (narrow stride-1 planes) == the LDS-tile kernel, bit for bit (same
+    fma order), and == float64 torch to 1e-6."""
+    from mlic_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    x = (torch.rand(B, Cn, H, W, generator=g) - 0.5).to(dev)
+    w = (torch.rand(Cn, 1, 3, 3, generator=g) - 0.5).to(dev)
+    b = (torch.rand(Cn, generator=g) - 0.5).to(dev)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = {}
+    for mode in (1, 0):
+        y = torch.full((B, Cn, H, W), float("nan"), device=dev)
+        _lib.call("mlic_set_kernel_option", b"dw_strip", mode)
+        try:
+            _lib.call("mlic_dw_run", C.c_void_p(st), C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()),
+                      C.c_void_p(b.data_ptr()), C.c_void_p(y.data_ptr()), B, Cn, H, W, 1, gelu)
+        finally:
+            _lib.call("mlic_set_kernel_option", b"dw_strip", -1)
+        outs[mode] = y
+    assert torch.equal(outs[0], outs[1])
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1, groups=Cn)
+    if gelu:
+        ref = F.gelu(ref)
+    check(outs[1], ref.float(), rtol=1e-6)
+
+
 @pytest.mark.parametrize("B,Cn,H,W,epi", [
     (2, 192, 40, 100, 1),    # GELU; 100 columns = one 60-column segment + a ragged 40
     (1, 192, 17, 61, 0),     # odd width: refused (the model runs it unfused)
