@@ -116,6 +116,9 @@ def parse():
     ap.add_argument("--split", type=int, default=0,
                     help="cut each (weights, shape) batch into this many request streams, each an independent "
                          "compress -> decompress chain on its own model instance (0: the workload's default)")
+    ap.add_argument("--schedule", choices=["join", "streams"], default="join",
+                    help="join: the batches of a step meet at a join every step; streams: when every batch has "
+                         "its own worker, each runs its K steps back to back")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="run rank --emulate-rank's share of a W-rank job list on this one GPU, with 1/W of "
                          "the host cores (a prediction of one rank of a W-GPU run; value = that rank's img/s)")
@@ -330,8 +333,25 @@ def main():
             split["compress"] += te
             split["decompress"] += td
 
-    for _ in range(a.warmup):
-        step()
+    # request streams (every batch has its own worker): each runs its n steps back to back, so the
+    # streams drift apart instead of meeting at a join every step; the timed region still holds exactly
+    # K steps of every batch, bracketed by the same synchronisation
+    streams_mode = a.schedule == "streams" and pool is not None and len(order) <= conc
+
+    def run_steps(n):
+        if not streams_mode:
+            for _ in range(n):
+                step()
+            return
+
+        def chain(gi):
+            return [run_group(gi) for _ in range(n)]
+        for res in pool.map(chain, order):
+            for te, td in res:
+                split["compress"] += te
+                split["decompress"] += td
+
+    run_steps(a.warmup)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -341,8 +361,7 @@ def main():
         _lib.call("mlic_host_stats", n._ensure_handle(dev), *[C.byref(v) for v in hs], 1)
     split["compress"] = split["decompress"] = 0.0
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    run_steps(a.steps)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -447,6 +466,8 @@ def main():
                                    f"rate set(s) {sorted({k[1] for k, _ in groups})} of synthetic.RATE_LAMBDAS"),
                        "parallelism": f"image-sharded x{world} (no cross-GPU context)",
                        "request_streams": len(groups), "lanes_per_stream": a.lanes,
+                       "schedule": ("each request stream runs its K steps back to back (no per-step join)"
+                                    if streams_mode else "batches joined every step"),
                        **({"synthesis": "fp16 operands (SURVEY f4)"} if a.synth_fp16 else {})},
             "roofline": roofline,
             **prof,

@@ -1175,7 +1175,7 @@ class PhaseDecoder {
         HostStats::Scope d{hs_->dec_ns};
         dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per);
       };
-      pool_->run(B, work);
+      pool_->run(B, work, HostPool::DECODE);
     }
     HIP_OK(hipMemcpyAsync(d_sym, h_sym_, sizeof(int32_t) * n_per * B, hipMemcpyHostToDevice, st));
   }
@@ -1734,7 +1734,7 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
       RansDecoderState dz;
       dz.set_stream(z[b], zlen[b]);
       dz.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
-    });
+    }, HostPool::DECODE);
   }
   PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool(), batch_stream);
   const int32_t* hz_sym = l.h_sym;

@@ -1,9 +1,14 @@
 // A fixed pool of host worker threads for the per-image entropy coding (rANS encode after the
 // network, rANS decode between the 20 slice phases).  Every lane submits its images' jobs here
 // instead of spawning threads per phase; run() blocks until the caller's batch is done and
-// rethrows the first exception of that batch.
+// rethrows the first exception of that batch.  Jobs are tagged encode / decode and, by default, the
+// encodes are served first: a lane's decompress cannot start before its images' streams exist, while
+// a queued per-phase decode only delays one lane's next small kernels (measured, 4 request streams x
+// 2 lanes, three alternating pairs: 89.5 img/s encodes-first against 88.4 FIFO; decodes-first 86.9
+// against FIFO 87.8).  $MLIC_POOL_PRIO: 2 (default) encodes first, 1 decodes first, 0 one FIFO.
 #pragma once
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
 #include <exception>
 #include <functional>
@@ -27,7 +32,8 @@ class HostPool {
     for (auto& t : workers_) t.join();
   }
   // runs fn(0..n-1) on the pool (the caller runs one share itself) and waits
-  void run(int n, const std::function<void(int)>& fn) {
+  enum Kind { ENCODE = 0, DECODE = 1 };
+  void run(int n, const std::function<void(int)>& fn, Kind kind = ENCODE) {
     if (n <= 1) {
       if (n == 1) fn(0);
       return;
@@ -41,8 +47,11 @@ class HostPool {
     batch.left = n - 1;
     {
       std::lock_guard<std::mutex> g(m_);
+      const int pr = prio();
+      const bool urgent = (pr == 1 && kind == DECODE) || (pr == 2 && kind == ENCODE);
+      auto& q = urgent ? uq_ : q_;
       for (int i = 1; i < n; ++i)
-        q_.push_back([&batch, &fn, i] {
+        q.push_back([&batch, &fn, i] {
           std::exception_ptr e;
           try {
             fn(i);
@@ -68,21 +77,29 @@ class HostPool {
   }
 
  private:
+  static int prio() {
+    static const int p = [] {
+      const char* e = std::getenv("MLIC_POOL_PRIO");
+      return e ? std::atoi(e) : 2;
+    }();
+    return p;
+  }
   void loop() {
     for (;;) {
       std::function<void()> job;
       {
         std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
-        if (stop_ && q_.empty()) return;
-        job = std::move(q_.front());
-        q_.pop_front();
+        cv_.wait(g, [this] { return stop_ || !q_.empty() || !uq_.empty(); });
+        if (stop_ && q_.empty() && uq_.empty()) return;
+        auto& q = uq_.empty() ? q_ : uq_;
+        job = std::move(q.front());
+        q.pop_front();
       }
       job();
     }
   }
   std::vector<std::thread> workers_;
-  std::deque<std::function<void()>> q_;
+  std::deque<std::function<void()>> q_, uq_;
   std::mutex m_;
   std::condition_variable cv_;
   bool stop_ = false;
