@@ -200,6 +200,10 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
     }
     float2v v = float2v{a0 + tw[9], a1 + tw[9]};
     if (MLIC_DPABL & 2) v = rk[1];  // diagnostics: no depthwise math
+    // the refill stays below the last read of the slot (as the chain kernel's input ring): hoisted
+    // above it, the loads land in fresh registers that the loop back-edge copies into the ring's --
+    // copies that wait for the loads (s_waitcnt vmcnt(0) at the end of every k-step)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
       rk[dy] = __builtin_bit_cast(float2v, __builtin_amdgcn_raw_buffer_load_b64(s.rs, s.vo[dy], so, 0));
@@ -279,7 +283,13 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
   };
   for (;;) {
     kstep(0, std::true_type{});
+#ifdef MLIC_DWPW_ROLLED  // A/B: the k-steps as a loop
 #pragma nounroll
+#else
+    // fully unrolled: a rolled loop's back-edge rotated the register ring with copies that waited for
+    // the ring's own refill loads (s_waitcnt vmcnt(0) closing every k-step)
+#pragma unroll
+#endif
     for (int j = 1; j < KS; ++j) kstep(j, std::false_type{});
 
     // epilogue (pw_resident's op sequence): bias, range guard, GELU, residual; pixel pairs as dwordx2

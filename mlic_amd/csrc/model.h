@@ -324,6 +324,7 @@ class Model {
   void planned(int B, hipStream_t st, F&& body);
   void ensure_host(size_t n);
   void ensure_chost(size_t n);
+  static int phase_d2h_mode();
   void set_vbr(const float* scales, int B);
 };
 
