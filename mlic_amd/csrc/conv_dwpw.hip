@@ -283,14 +283,17 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
   };
   for (;;) {
     kstep(0, std::true_type{});
-#ifdef MLIC_DWPW_ROLLED  // A/B: the k-steps as a loop
-#pragma nounroll
-#else
-    // fully unrolled: a rolled loop's back-edge rotated the register ring with copies that waited for
-    // the ring's own refill loads (s_waitcnt vmcnt(0) closing every k-step)
+    // the rolled loop's back-edge rotates the register ring with copies that wait for the ring's own
+    // refill loads (s_waitcnt vmcnt(0) closing every k-step).  Fully unrolled, the bias-only form runs
+    // 2.30 instead of 2.42 ms (8 x 192 x 544 x 960); the GELU forms do not gain (GELU 2.38 / 2.35, GELU +
+    // residual 3.33 / 2.93: the unrolled body spills SGPRs into lanes), so they keep the loop
+    if constexpr (MODE == 0 && !RES) {
 #pragma unroll
-#endif
-    for (int j = 1; j < KS; ++j) kstep(j, std::false_type{});
+      for (int j = 1; j < KS; ++j) kstep(j, std::false_type{});
+    } else {
+#pragma nounroll
+      for (int j = 1; j < KS; ++j) kstep(j, std::false_type{});
+    }
 
     // epilogue (pw_resident's op sequence): bias, range guard, GELU, residual; pixel pairs as dwordx2
     {
