@@ -218,7 +218,12 @@ class EntropyBottleneck(EntropyModel):
         return logits
 
     def _likelihood(self, inputs):
-        # compressai 1.2.x: plain sigmoid difference
+        # compressai 1.2.x: plain sigmoid difference.  PARITY UNPINNED: compressai is not installed here
+        # and nothing in the reference tree holds its output; the form restated is 1.2.6's
+        # EntropyBottleneck._likelihood as published -- lower = self._logits_cumulative(inputs - half),
+        # upper = self._logits_cumulative(inputs + half), likelihood = sigmoid(upper) - sigmoid(lower)
+        # (1.1.x instead took sign = -sign(lower + upper) and abs(sigmoid(sign * upper) - sigmoid(sign *
+        # lower))); update() builds the pmf from the same expression with stop_gradient=True
         half = float(0.5)
         lower = self._logits_cumulative(inputs - half, stop_gradient=False)
         upper = self._logits_cumulative(inputs + half, stop_gradient=False)
