@@ -424,13 +424,23 @@ void Model::add_hoist(const std::map<std::string, std::pair<const float*, int>>&
   HIP_OK(hipFree(tmp));
 }
 
-// $MLIC_HOIST=0: EntropyParameters consume hyper_params inside each chain (A/B switch)
+// Whether EntropyParameters' hyper columns run as the one hoisted GEMM before the slice loop.  Default
+// (auto): only when some EP's full input (context + hyper) cannot take the fused chain (an odd number of
+// 32-channel chunks: MLICPP_M_SMALL_DEC's 2 hM = 160); otherwise every chain consumes hyper_params
+// itself -- the chain kernel is VALU-bound with MFMA to spare, and the hoisted 640 -> 6400 GEMM costs
+// ≈ 2 ms per 8 images on each side (measured, main config, alternating pairs on one box: 91.4 vs 89.9
+// img/s).  $MLIC_HOIST=1 / 0 forces it on / off (A/B).
 bool Model::hoist_on() const {
-  static const bool on = [] {
+  static const int env = [] {
     const char* e = std::getenv("MLIC_HOIST");
-    return !(e && std::atoi(e) == 0);
+    return e ? std::atoi(e) : -1;
   }();
-  return on && chain_on() && hoist_.Cout > 0;
+  bool want = env >= 0 ? env != 0 : false;
+  if (env < 0)
+    for (int i = 0; i < cfg_.S && !want; ++i)
+      for (const char* k : {"anchor", "nonanchor"})
+        if (!chains_.count(std::string("entropy_parameters_") + k + "." + std::to_string(i) + ".fusion")) want = true;
+  return want && chain_on() && hoist_.Cout > 0;
 }
 
 // the fused dwpw kernel (conv_dwpw.hip) instead of depthwise + resident pointwise for the stride-1
