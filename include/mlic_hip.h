@@ -101,7 +101,9 @@ int mlic_set_poison(mlic_model* m, int on);
  * halo-staged B operand for K x K stride-1 convs (1 on, 0 off, -1 default = $MLIC_X4_HALO or on);
  * "linatt_fused" = the linear attention's output written straight into the
  * reprojection conv's packed operand ($MLIC_LINATT_FUSED); "dw_strip" = the register-strip depthwise
- * 3x3 for stride-1 planes up to 64 columns ($MLIC_DW_STRIP) */
+ * 3x3 for stride-1 planes up to 64 columns ($MLIC_DW_STRIP); "x4_splitk" = split-K for few-tile
+ * 3x3 / 5x5 convs (default off, $MLIC_X4_SPLITK=1) -- set it before a handle's first call (the
+ * workspace is sized for the setting in force then) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
  * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the

@@ -906,11 +906,19 @@ static void launch_x4(const ConvParams& P, const _Float16* act, const _Float16* 
 // of one Cout tile, 1.1 waves of blocks over the CUs at 8 images) with a long K loop is cut into
 // nsplit K ranges whose partial sums a combine kernel adds in a fixed order.  A function of the
 // per-image shape only: the result bits must not depend on the batch (encoder = decoder).
+// Round 4: OFF by default.  Alone on the GPU a split launch is faster, but the timed configuration
+// keeps 8 lanes of kernels in flight, which fill the CUs those few-tile launches leave idle, and the
+// split adds a partial-sum pass and a combine launch: main config 91.1 / 91.6 img/s without against
+// 90.2 / 90.3 with (alternating, one box); Kodak-size and MLICPP_M_SMALL_DEC within noise.
+// $MLIC_X4_SPLITK=1 or mlic_set_kernel_option("x4_splitk", 1) turns it on (tests, A/B).
+static int g_x4_splitk = -1;
+void x4_set_splitk(int v) { g_x4_splitk = v; }
 int x4_splitk(const ConvParams& P, int cin_pad, bool hi) {
-  static const bool on = [] {  // $MLIC_X4_SPLITK=0: no split (A/B switch)
+  static const bool env_on = [] {
     const char* e = std::getenv("MLIC_X4_SPLITK");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) != 0;
   }();
+  const bool on = g_x4_splitk >= 0 ? g_x4_splitk != 0 : env_on;
   if (!on || !x4_rs() || P.K == 1) return 1;
   int H, W;
   x4_tgrid(P, H, W);

@@ -124,7 +124,8 @@ struct DwParams {
   int B;
 };
 void dw3x3(const DwParams& P, hipStream_t st);
-void dw_set_strip(int v);  // A/B: 0 = the LDS-tile kernel for narrow stride-1 planes too
+void dw_set_strip(int v);
+void x4_set_splitk(int v);  // -1 default ($MLIC_X4_SPLITK, off), 0 off, 1 on  // A/B: 0 = the LDS-tile kernel for narrow stride-1 planes too
 
 void ln_channels(const float* x, int64_t x_bs, float* y, int64_t y_bs, const float* g, const float* b, int C,
                  int HW, int B, hipStream_t st);

@@ -209,22 +209,27 @@ def test_x4(shape):
 def test_x4_halo_vs_per_tap(shape):
     """conv_x4's halo-staged B operand (one (8+K-1) x (32+K-1) image per 32-channel chunk, every tap a
     shifted read of it) against B staged per tap: the same operands in the same MFMA order, so the
-    outputs are bit-identical whenever the K loop is not split; with split-K (few-tile shapes) the
-    halo form splits on chunk boundaries, so both are only checked against float64."""
+    outputs are bit-identical when the K loop is not split (the default); with split-K forced on
+    (few-tile shapes) the halo form splits on chunk boundaries, so both are checked against float64
+    and against the unsplit result to the float64 tolerance."""
     from mlic_amd import _lib
     B, cin, cout, H, W, K, epi = shape
+    res = {}
     try:
-        _lib.call("mlic_set_kernel_option", b"x4_halo", 1)
-        y1, ref = run(X4, B, cin, cout, H, W, K, epi=epi)
-        _lib.call("mlic_set_kernel_option", b"x4_halo", 0)
-        y0, _ = run(X4, B, cin, cout, H, W, K, epi=epi)
+        for split in (0, 1):
+            _lib.call("mlic_set_kernel_option", b"x4_splitk", split)
+            for halo in (1, 0):
+                _lib.call("mlic_set_kernel_option", b"x4_halo", halo)
+                res[(split, halo)] = run(X4, B, cin, cout, H, W, K, epi=epi)
     finally:
         _lib.call("mlic_set_kernel_option", b"x4_halo", -1)
-    check(y1, ref)
-    check(y0, ref)
+        _lib.call("mlic_set_kernel_option", b"x4_splitk", -1)
+    for (y, ref) in res.values():
+        check(y, ref)
+    assert torch.equal(res[(0, 1)][0], res[(0, 0)][0])  # no split: halo == per-tap, bit for bit
     tiles = -(-cout // 256) * -(-W // 32) * -(-H // 8)
-    if tiles > 48:  # no split-K (conv_x4.hip x4_splitk)
-        assert torch.equal(y1, y0)
+    if tiles > 48:  # split-K never applies (conv_x4.hip x4_splitk): forced on changes nothing
+        assert torch.equal(res[(1, 1)][0], res[(0, 1)][0])
 
 
 def _conv_raw(impl, x, w, b, epi):
