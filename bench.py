@@ -71,7 +71,9 @@ WORKLOADS = {
                   desc="config 1 shape on GPU: MLICPP_L compress+decompress of 768x512 (Kodak-size) images"),
     "s1080": dict(model="MLICPP_S", groups=[(1088, 1920, 32)], scaling="weak",
                   desc="config 3: MLICPP_S compress+decompress of 1920x1088 images"),
-    "sd1080": dict(model="MLICPP_M_SMALL_DEC", groups=[(1088, 1920, 32)], scaling="weak",
+    # (request streams: sd1080 88.9-89.2 vs 88.0-88.3 img/s; MLICPP_S and the Kodak-size batch do not
+    # gain -- 223-227 either way, and 392-405 against 460-462 for Kodak-size)
+    "sd1080": dict(model="MLICPP_M_SMALL_DEC", groups=[(1088, 1920, 32)], scaling="weak", split=4, lanes=2,
                    desc="config 3: MLICPP_M_SMALL_DEC compress+decompress of 1920x1088 images"),
     # the sweep's 12 (rate, shape) batches of 4-20 Kodak-size images fill the GPU best as 6 concurrent
     # batches of 2 lanes each (measured: 310 img/s vs 224 with 4 x 4, 194 with 6 x 4, 249 with 12 x 2)
