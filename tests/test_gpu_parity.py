@@ -149,6 +149,9 @@ def test_forward_matches_reference_fixture(golden, name, H, W, s):
     p_ref = ref.psnr_uint8(x, torch.from_numpy(g["x_hat"]))
     p_gpu = ref.psnr_uint8(x, out["x_hat"].cpu())
     assert abs(p_gpu - p_ref) <= 0.01, (p_gpu, p_ref)
+    d = (out["x_hat"].cpu().float() - torch.as_tensor(np.asarray(g["x_hat"])).float()).abs()
+    PARITY[f"fixture_forward_{tag}"] = {"xhat_max_abs_err": float(d.max()), "xhat_mean_abs_err": float(d.mean()),
+                                        "xhat_psnr_vs_ref_db": _psnr_f(out["x_hat"].cpu(), g["x_hat"])}
     assert_xhat_close(out["x_hat"].cpu(), g["x_hat"])
     assert maxdiff(out["likelihoods"]["z_likelihoods"].cpu(), g["z_lik"]) <= 1e-4
 
