@@ -152,7 +152,9 @@ def test_forward_matches_reference_fixture(golden, name, H, W, s):
     d = (out["x_hat"].cpu().float() - torch.as_tensor(np.asarray(g["x_hat"])).float()).abs()
     PARITY[f"fixture_forward_{tag}"] = {"xhat_max_abs_err": float(d.max()), "xhat_mean_abs_err": float(d.mean()),
                                         "xhat_psnr_vs_ref_db": _psnr_f(out["x_hat"].cpu(), g["x_hat"])}
-    assert_xhat_close(out["x_hat"].cpu(), g["x_hat"])
+    # against the reference's own outputs no latent rounds differently on these fixtures (measured
+    # max 1.1e-6 over all of them, profiles/r04/parity_counts.json): every pixel within 1e-4
+    assert float(d.max()) <= 1e-4, float(d.max())
     assert maxdiff(out["likelihoods"]["z_likelihoods"].cpu(), g["z_lik"]) <= 1e-4
 
 
