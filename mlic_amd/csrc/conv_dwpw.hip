@@ -65,6 +65,9 @@ __device__ __forceinline__ int dr_swz(int row) { return (row >> 2) & 3; }
 
 }  // namespace
 
+#ifndef MLIC_DWPW_ROLLED_ALL  // A/B build: 1 = the k-steps of the bias-only form as a loop too
+#define MLIC_DWPW_ROLLED_ALL 0
+#endif
 #ifndef MLIC_DPABL  // diagnostics build: 1 = one MFMA per k-step, 2 = no depthwise math, 4 = no output stores
 #define MLIC_DPABL 0
 #endif
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
     // refill loads (s_waitcnt vmcnt(0) closing every k-step).  Fully unrolled, the bias-only form runs
     // 2.30 instead of 2.42 ms (8 x 192 x 544 x 960); the GELU forms do not gain (GELU 2.38 / 2.35, GELU +
     // residual 3.33 / 2.93: the unrolled body spills SGPRs into lanes), so they keep the loop
-    if constexpr (MODE == 0 && !RES) {
+    if constexpr (MODE == 0 && !RES && !MLIC_DWPW_ROLLED_ALL) {
 #pragma unroll
       for (int j = 1; j < KS; ++j) kstep(j, std::false_type{});
     } else {
