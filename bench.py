@@ -76,8 +76,10 @@ WORKLOADS = {
     "sd1080": dict(model="MLICPP_M_SMALL_DEC", groups=[(1088, 1920, 32)], scaling="weak", split=4, lanes=2,
                    desc="config 3: MLICPP_M_SMALL_DEC compress+decompress of 1920x1088 images"),
     # the sweep's 12 (rate, shape) batches of 4-20 Kodak-size images fill the GPU best as 6 concurrent
-    # batches of 2 lanes each (measured: 310 img/s vs 224 with 4 x 4, 194 with 6 x 4, 249 with 12 x 2)
-    "kodak-sweep": dict(model="MLICPP_L", scaling="strong", lanes=2, group_concurrency=6,
+    # batches of 1 lane each (round 4, alternating: 425.7 / 428.0 img/s against 308.4 / 325.1 with 2 lanes,
+    # 411.9 / 424.0 with 8 x 1); a rank holding a single batch (rank 0 of 8: 18 images) keeps 2 lanes
+    # (322.6 / 322.8 against 299.9 with 1)
+    "kodak-sweep": dict(model="MLICPP_L", scaling="strong", lanes=2, lanes_many=1, group_concurrency=6,
                         desc="config 4: MLICPP_L 24 Kodak-size images x 6 lambda stand-ins, LPT-sharded"),
     # (4 request streams of 1-3 images, 2 lanes each: 40.2-40.4 img/s against 39.4-39.6 as two batches)
     "vbr-mixed": dict(model="MLICPP_L_VBR", groups=[(2176, 3840, 2), (1088, 1920, 6)], scaling="weak", split=2, lanes=2,
@@ -128,6 +130,7 @@ def parse():
     ap.add_argument("--emulate-rank", type=int, default=0)
     a = ap.parse_args()
     wl = WORKLOADS[a.config]
+    a.lanes_auto = a.lanes <= 0 and "MLIC_LANES" not in os.environ and "lanes_many" in wl
     if a.lanes <= 0:
         a.lanes = int(os.environ["MLIC_LANES"]) if "MLIC_LANES" in os.environ else wl.get("lanes", 4)
     if a.group_concurrency <= 0:
@@ -287,6 +290,9 @@ def main():
     # biggest batches first: the concurrent groups finish together
     order = sorted(range(len(groups)), key=lambda gi: -len(groups[gi][1]) * groups[gi][0][2] * groups[gi][0][3])
     conc = max(1, min(a.group_concurrency, len(groups)))
+    if a.lanes_auto and len(groups) >= conc and conc > 1:
+        # more batches than concurrent slots: the batches overlap each other, one lane each is best
+        a.lanes = WORKLOADS[a.config]["lanes_many"]
 
     # one model instance per group when groups run concurrently (a handle's lanes serve one call at a
     # time), one per weight set otherwise
