@@ -132,3 +132,25 @@ def test_kodak_sweep_sharded_world2():
         j = int(r[0])
         assert int(r[3]) == j // 24  # lambda level
         assert (int(r[1]), int(r[2])) == ((512, 768) if j % 24 < 20 else (768, 512))
+
+
+def test_request_streams_cover_the_batch():
+    """bench.py --split: the main config's 32 images per rank become 4 request streams of 8 (each its
+    own model instance at run time), every job exactly once; the VBR config's two batches become 4
+    streams; split 1 keeps one batch per (weights, shape)."""
+    import argparse
+    import bench
+    for world, rank in ((1, 0), (8, 3)):
+        a = argparse.Namespace(config="main", rate=1, batch=0)
+        jobs, total = bench.build_jobs(a, rank, world)
+        assert total == 32 * world and len(jobs) == 32
+        for split, want in ((4, [8, 8, 8, 8]), (1, [32]), (3, [11, 11, 10])):
+            groups = bench.batches(jobs, split=split)
+            assert [len(js) for _, js in groups] == want
+            ids = sorted(j.id for _, js in groups for j in js)
+            assert ids == sorted(j.id for j in jobs)
+    a = argparse.Namespace(config="vbr-mixed", rate=1, batch=0)
+    jobs, _ = bench.build_jobs(a, 0, 1)
+    groups = bench.batches(jobs, split=bench.WORKLOADS["vbr-mixed"]["split"])
+    assert sorted(len(js) for _, js in groups) == [1, 1, 3, 3]
+    assert sorted(j.id for _, js in groups for j in js) == sorted(j.id for j in jobs)
