@@ -87,7 +87,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -128,7 +128,10 @@ def parse():
                     help="run rank --emulate-rank's share of a W-rank job list on this one GPU, with 1/W of "
                          "the host cores (a prediction of one rank of a W-GPU run; value = that rank's img/s)")
     ap.add_argument("--emulate-rank", type=int, default=0)
-    a = ap.parse_args()
+    ap.add_argument("--phase", choices=["both", "decode"], default="both",
+                    help="both: a step = compress + decompress (the metric's enc+dec); decode: a step = "
+                         "decompress() of streams encoded before the timed region (north_star's decode target)")
+    a = ap.parse_args(argv)
     wl = WORKLOADS[a.config]
     a.lanes_auto = a.lanes <= 0 and "MLIC_LANES" not in os.environ and "lanes_many" in wl
     if a.lanes <= 0:
@@ -203,33 +206,73 @@ def mse_u8(a: torch.Tensor, b: torch.Tensor):
 
 
 # ------------------------------------------------------------------------------------------ CPU side
-def cpu_baseline(model: str, rate, H: int, W: int, level: int = -1):
+def _cpu_thread_choice(candidates, probe):
+    """Time `probe` (a short slice of the same oracle work) at each thread count; the fastest wins.
+    The box's core count is not the box's best thread count: a GPU box may give one GPU's process a
+    share of a much larger host, so the choice is measured, not assumed."""
+    times = {}
+    for n in candidates:
+        torch.set_num_threads(n)
+        probe()  # warm the thread pool at this size
+        t0 = time.perf_counter()
+        probe()
+        times[n] = time.perf_counter() - t0
+    best = min(times, key=times.get)
+    return best, {str(k): round(v, 4) for k, v in times.items()}
+
+
+def cpu_baseline(model: str, rate, H: int, W: int, level: int = -1, phase: str = "both", seed: int = 0):
     """Oracle (torch CPU fp32 restatement of the reference) enc+dec of one image, with the native
-    rANS coder for the entropy-coding part; threads = this process's CPU affinity (<= 32)."""
+    rANS coder for the entropy-coding part, on the best thread count of this box's cores (measured
+    over 16 / 32 / 64 / all of this process's affinity on a short g_a probe, then the whole image at that
+    count).  Returns the baseline record and the oracle's own coding result of that image (bytes,
+    likelihood bpp, x_hat) for the headline's delta (`quality.delta_vs_cpu_oracle`)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import mlic_ref_cpu as ref
-    from mlic_amd import entropy, synthetic
-    cores = max(1, min(32, len(os.sched_getaffinity(0))))
-    torch.set_num_threads(cores)
+    from mlic_amd import bitstream, entropy, synthetic
+    aff = len(os.sched_getaffinity(0))
+    total = os.cpu_count() or aff
     sd = synthetic.synth_state_dict(model, 0, rate=rate)
     m = ref.RefMLIC(model, sd)
-    x = synthetic.synth_image(H, W, 0)
+    x = synthetic.synth_image(H, W, seed)
     s = max(0, level)
+    xp = x[:, :, :256, :512].contiguous()
+    cands = sorted({c for c in (16, 32, 64, aff) if c <= aff} or {aff})
+    threads, probe_s = _cpu_thread_choice(cands, lambda: m.g_a(xp))
+    torch.set_num_threads(threads)
     tables = entropy.gaussian_tables(entropy.get_scale_table())
+    eb = {k.split(".", 1)[1]: v for k, v in sd.items() if k.startswith("entropy_bottleneck.")}
+    etab = entropy.bottleneck_tables(eb)
     t0 = time.time()
-    st = m.compress_streams(x, s=s)
+    st = m.compress_streams(x, s=s, likelihoods=True)
     sym = torch.cat([p[0].reshape(-1) for p in st["phases"]]).numpy()
     idx = torch.cat([p[1].reshape(-1) for p in st["phases"]]).numpy()
     data = entropy.rans_encode(sym, idx, *tables[:3])
+    zs = st["z_symbols"]
+    zidx = np.broadcast_to(np.arange(zs.shape[1], dtype=np.int32)[:, None, None], zs.shape[1:]).reshape(-1)
+    zdata = entropy.rans_encode(zs.reshape(-1).numpy(), zidx, *etab)
+    t1 = time.time()
     dec = entropy.rans_decode(data, idx, *tables[:3])
+    zdec = entropy.rans_decode(zdata, zidx, *etab).reshape(zs.shape)
     offs = np.cumsum([0] + [p[0].numel() for p in st["phases"]])
     phase_syms = [torch.from_numpy(dec[offs[k]:offs[k + 1]]).reshape(st["phases"][k][0].shape)
                   for k in range(len(st["phases"]))]
-    m.decode_streams(st["z_symbols"], phase_syms, s=s)
-    dt = time.time() - t0
-    return {"value": round(1.0 / dt, 5), "unit": "images/sec (enc+dec)", "cores": cores, "kind": "port",
-            "sample": f"1 image {W}x{H} {model} (rate set {rate}): oracle torch-CPU fp32 encoder+decoder "
-                      f"networks + native rANS, {dt:.1f} s"}
+    x_hat = m.decode_streams(torch.from_numpy(zdec), phase_syms, s=s)["x_hat"]
+    t2 = time.time()
+    dt = (t2 - t1) if phase == "decode" else (t2 - t0)
+    lik = st["likelihoods"]
+    nbytes = bitstream.file_bytes(len(data), len(zdata), vbr=level >= 0)
+    coded = {"bytes": nbytes, "bpp_file": 8.0 * nbytes / (H * W),
+             "bpp_lik": ref.bpp_from_likelihoods(lik["y_likelihoods"], lik["z_likelihoods"], H * W),
+             "psnr": ref.psnr_uint8(x, x_hat), "H": H, "W": W}
+    what = "decoder network + native rANS decode" if phase == "decode" else "encoder+decoder networks + native rANS"
+    rec = {"value": round(1.0 / dt, 5), "unit": "images/sec (decode)" if phase == "decode" else "images/sec (enc+dec)",
+           "cores": threads, "threads_used": threads, "cores_total": total, "cores_affinity": aff,
+           "thread_probe_s": probe_s, "kind": "port",
+           "sample": f"1 image {W}x{H} {model} (rate set {rate}, seed {seed}: a GPU job's image): oracle torch-CPU fp32 {what}, "
+                     f"{dt:.1f} s on {threads} threads (best of {cands} on a g_a probe; {total} host cores, "
+                     f"{aff} in this process's affinity)"}
+    return rec, coded
 
 
 def oracle_deltas(model: str, levels, H: int, W: int, gpu_nets, dev):
@@ -252,9 +295,48 @@ def oracle_deltas(model: str, levels, H: int, W: int, gpu_nets, dev):
     return out
 
 
+# ------------------------------------------------------------------------------- timing + collectives
+def timed_steps(run_steps, steps: int, distributed: bool, dev, sync=None) -> float:
+    """The timed region: barrier + device sync on both sides of exactly `steps` steps; returns the
+    elapsed seconds, max over ranks (all_reduce MAX on `dev`: RCCL on the GPU box, gloo in the CPU
+    test).  `sync` is torch.cuda.synchronize on a GPU."""
+    sync = sync or (lambda: None)
+    sync()
+    if distributed:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run_steps(steps)
+    sync()
+    if distributed:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_all(rec: torch.Tensor, n_expected: int, distributed: bool, dev) -> torch.Tensor:
+    """The one data collective: every rank's fixed-size per-image records, all_gathered (padded to the
+    largest rank's count, agreed by an all_reduce MAX) and sorted by job; asserts that every job of the
+    list is there exactly once."""
+    from mlic_amd import dist as mdist
+    max_per_rank = max(rec.shape[0], 1)
+    if distributed:
+        mx = torch.tensor([max_per_rank], device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        max_per_rank = int(mx.item())
+    allrec = mdist.gather_records(rec.to(dev), max_per_rank=max_per_rank).cpu()
+    ids = allrec[:, 0].long().tolist()
+    assert len(ids) == n_expected and len(set(ids)) == n_expected, (len(ids), len(set(ids)), n_expected)
+    return allrec
+
+
 # ------------------------------------------------------------------------------------------ main
-def main():
-    a = parse()
+def main(argv=None):
+    a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -317,14 +399,26 @@ def main():
 
     split = {"compress": 0.0, "decompress": 0.0}
     last = {}
+    decode_only = a.phase == "decode"
+
+    def group_kw(gi):
+        return {"stage": 2, "s": [j.level for j in groups[gi][1]]} if is_vbr else {}
+
+    # decode phase: every group's streams are encoded once, before the warmup and the timed region
+    pre = {}
+    if decode_only:
+        for gi in range(len(groups)):
+            with torch.cuda.stream(streams[gi]):
+                pre[gi] = gnet[gi].compress(xs[gi], **group_kw(gi))
+        torch.cuda.synchronize()
 
     def run_group(gi):
-        (model, rate, H, W), js = groups[gi]
+        js = groups[gi][1]
         net = gnet[gi]
-        kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
+        kw = group_kw(gi)
         with torch.cuda.stream(streams[gi]):
             t_a = time.perf_counter()
-            c = net.compress(xs[gi], **kw)
+            c = pre[gi] if decode_only else net.compress(xs[gi], **kw)
             t_b = time.perf_counter()
             d = net.decompress(c["strings"], c["shape"], **kw)
             t_c = time.perf_counter()
@@ -362,20 +456,11 @@ def main():
 
     run_steps(a.warmup)
     torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
     hs = [C.c_double() for _ in range(3)]
     for n in nets.values():
         _lib.call("mlic_host_stats", n._ensure_handle(dev), *[C.byref(v) for v in hs], 1)
     split["compress"] = split["decompress"] = 0.0
-    t0 = time.perf_counter()
-    run_steps(a.steps)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_steps(run_steps, a.steps, distributed, dev, sync=torch.cuda.synchronize)
     host = {"rans_encode": 0.0, "rans_decode": 0.0, "gpu_wait": 0.0}
     for n in nets.values():
         _lib.call("mlic_host_stats", n._handle, *[C.byref(v) for v in hs], 1)
@@ -383,10 +468,8 @@ def main():
             host[k] += v.value / a.steps
     host = {k: round(v, 2) for k, v in host.items()}
     wall_split = {k: round(1000 * v / a.steps, 2) for k, v in split.items()}
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    if decode_only:
+        wall_split.pop("compress")
 
     # per-image records (mlic_amd.dist.RECORD_FIELDS): the one collective, all_gather over RCCL/xGMI
     F = {k: i for i, k in enumerate(mdist.RECORD_FIELDS)}
@@ -399,8 +482,7 @@ def main():
         if gnet.count(net) > 1:
             # the device-side likelihood bits belong to a net's last compress(): groups sharing one
             # net (vbr-mixed's 4K + 1080p) re-run this group's compress, untimed, to read them
-            kw = {"stage": 2, "s": [j.level for j in js]} if is_vbr else {}
-            c = net.compress(xs[gi], **kw)
+            c = net.compress(xs[gi], **group_kw(gi))
         for i, j in enumerate(js):
             # the file the harness writes (header included, utils/utils.py:71-83), as bitstream.write_stream
             nbytes = bitstream.file_bytes(len(c["strings"][0][i]), len(c["strings"][1][i]), vbr=is_vbr)
@@ -416,14 +498,8 @@ def main():
             rec[r, F["enc_ms"]] = 1000 * enc_s
             rec[r, F["dec_ms"]] = 1000 * dec_s
             r += 1
-    max_per_rank = max(len(jobs), 1)
-    if distributed:
-        mx = torch.tensor([max_per_rank], device=dev)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        max_per_rank = int(mx.item())
-    allrec = mdist.gather_records(rec.to(dev), max_per_rank=max_per_rank).cpu()
     # every job of the list exactly once (emulated: this rank's share of it)
-    assert allrec.shape[0] == (len(jobs) if emulated else n_jobs_total), (allrec.shape, n_jobs_total)
+    allrec = gather_all(rec, len(jobs) if emulated else n_jobs_total, distributed, dev)
 
     # live roofline: extra profiled (untimed) steps.  Pass 1 runs the timed steps' lane count, so its
     # per-launch averages are what rocprofv3 sees over the whole run (concurrent lanes stretch each
@@ -432,7 +508,8 @@ def main():
     roofline = None
     prof = {}
     if not a.no_roofline:
-        roofline, prof = profile_roofline(a, gnet, groups, xs, is_vbr, elapsed / a.steps, dev)
+        roofline, prof = profile_roofline(a, gnet, groups, xs, is_vbr, elapsed / a.steps, dev,
+                                          pre=pre if decode_only else None)
 
     if rank == 0:
         if emulated:  # this rank's images only: a per-GPU prediction
@@ -454,7 +531,10 @@ def main():
             quality["per_level"] = per
         cfg0 = groups[0][0]
         out = {
-            "metric": METRIC if a.config == "main" else f"images/sec (enc+dec), {wl['desc']}",
+            "metric": (METRIC if a.config == "main" else f"images/sec (enc+dec), {wl['desc']}") if not decode_only
+                      else f"images/sec (decode only: decompress() of streams encoded before the timed region), "
+                           f"{wl['desc']}",
+            "phase": a.phase,
             "value": round(images / elapsed, 4),
             "unit": "images/sec",
             "n_gpus": world,
@@ -495,9 +575,28 @@ def main():
                                "note": "one rank's job list of a W-GPU run on one GPU with 1/W of the host cores; "
                                        "value = that rank's images/s (per-GPU)"}
         if world == 1 and not a.no_cpu_baseline:
-            j0 = jobs[0]
-            sH, sW = (j0.H, j0.W) if j0.H * j0.W <= 1088 * 1920 else (1088, 1920)
-            out["cpu_baseline"] = cpu_baseline(j0.model, j0.rate, sH, sW, j0.level if is_vbr else -1)
+            # the CPU sample is one of the GPU's own jobs (the first of at most 1080p size): the oracle
+            # codes that image, so the headline carries the bpp / PSNR delta against the CPU path on the
+            # same input (BASELINE metric "bpp/PSNR delta vs ref"; loss/rd_loss.py:42-45, utils/metrics.py:32-33)
+            j0 = next((j for j in jobs if j.H * j.W <= 1088 * 1920), jobs[0])
+            out["cpu_baseline"], coded = cpu_baseline(j0.model, j0.rate, min(j0.H, 1088), min(j0.W, 1920),
+                                                      j0.level if is_vbr else -1, phase=a.phase, seed=j0.seed)
+            g0 = q[q[:, F["job"]] == j0.id][0]
+            if (coded["H"], coded["W"]) == (j0.H, j0.W):
+                d_lik = float(g0[F["bpp_lik"]]) - coded["bpp_lik"]
+                d_psnr = float(g0[F["psnr"]]) - coded["psnr"]
+                out["quality"]["delta_vs_cpu_oracle_job"] = {
+                    "job": j0.id, "image": f"{j0.W}x{j0.H} seed {j0.seed}, rate set {j0.rate}"
+                                           + (f", VBR level {j0.level}" if is_vbr else ""),
+                    "bpp_lik_gpu": round(float(g0[F["bpp_lik"]]), 7), "bpp_lik_cpu": round(coded["bpp_lik"], 7),
+                    "d_bpp_lik": round(d_lik, 8),
+                    "bpp_file_gpu": round(float(g0[F["bpp_file"]]), 7), "bpp_file_cpu": round(coded["bpp_file"], 7),
+                    "d_bpp_file": round(float(g0[F["bpp_file"]]) - coded["bpp_file"], 8),
+                    "psnr_gpu": round(float(g0[F["psnr"]]), 6), "psnr_cpu": round(coded["psnr"], 6),
+                    "d_psnr_db": round(d_psnr, 7),
+                    "within_tolerance": bool(abs(d_lik) <= 1e-3 and abs(d_psnr) <= 1e-2),
+                    "tolerance": "north_star: |d bpp| <= 0.001, |d PSNR| <= 0.01 dB (GPU: the timed run's own "
+                                 "bitstream and decoded x_hat; CPU: the oracle's encoder, native rANS and decoder)"}
             if a.config == "kodak-sweep":
                 out["quality"]["delta_vs_cpu_oracle"] = oracle_deltas(
                     wl["model"], sorted({k[1] for k, _ in groups}), 512, 768,
@@ -513,7 +612,8 @@ def main():
         dist.destroy_process_group()
 
 
-def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev):
+def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev, pre=None):
+    """pre: the decode phase's pre-encoded streams per group (only decompress launches are counted)."""
     from mlic_amd import _lib
     ncat = C.c_int()
     _lib.call("mlic_profile_categories", C.byref(ncat))
@@ -554,9 +654,16 @@ def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev):
                     f["flops"] += fl.value
                     f["bytes"] += by.value
 
-            c = net.compress(x, **kw)
-            torch.cuda.synchronize()
-            harvest("compress")
+            if pre is None:
+                c = net.compress(x, **kw)
+                torch.cuda.synchronize()
+                harvest("compress")
+            else:  # decode phase: the streams of the timed steps (the isolated pass: its first images')
+                c = pre[gi] if share is None else net.compress(x, **kw)
+                torch.cuda.synchronize()
+                for cat in range(ncat.value):  # drop the encoder's launches
+                    _lib.call("mlic_profile_read", h, cat, *[C.byref(v) for v in (C.c_int64(), C.c_double(),
+                                                                                  C.c_double(), C.c_double())])
             net.decompress(c["strings"], c["shape"], **kw)
             torch.cuda.synchronize()
             harvest("decompress")

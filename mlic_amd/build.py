@@ -47,13 +47,30 @@ def _sha256(path: str) -> str:
     return h.hexdigest()
 
 
-def build(jobs: int = 8, verbose: bool = False) -> str:
+def build(jobs: int = 8, verbose: bool = False, incremental: bool = None) -> str:
+    """Compile the library.  By default from clean (the object directory is removed first, ~90 s on 8
+    cores), so the record proves that the sources of this tree compile into this library; the
+    developer loop passes incremental=True (or sets $MLIC_BUILD_INCREMENTAL=1) and make rebuilds only
+    what changed.  The record says which it was and how many objects were compiled."""
+    import shutil
+    import time
+    if incremental is None:
+        incremental = os.environ.get("MLIC_BUILD_INCREMENTAL", "0") not in ("", "0")
     csrc = os.path.join(HERE, "csrc")
+    objdir = os.path.join(csrc, "build")
+    if not incremental and os.path.isdir(objdir):
+        shutil.rmtree(objdir)
     cmd = ["make", "-C", csrc, f"-j{jobs}", "OUT=" + LIB]
-    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if verbose:
+        sys.stdout.write(r.stdout or "")
+        sys.stderr.write(r.stderr or "")
     if r.returncode != 0:
         sys.stderr.write((r.stdout or "") + (r.stderr or ""))
         raise RuntimeError("building libmlic_hip.so failed")
+    compiled = sum(1 for ln in (r.stdout or "").splitlines() if " -c " in ln and "hipcc" in ln)
+    linked = any("-shared" in ln for ln in (r.stdout or "").splitlines())
     try:
         hipcc = subprocess.run(["/opt/rocm/bin/hipcc", "--version"], capture_output=True, text=True).stdout
         hipcc = next((ln.strip() for ln in hipcc.splitlines() if "HIP version" in ln), hipcc.strip()[:80])
@@ -62,11 +79,21 @@ def build(jobs: int = 8, verbose: bool = False) -> str:
     rec = {"library": os.path.basename(LIB), "library_sha256": _sha256(LIB), "sources_sha256": source_digest(),
            "sources": [os.path.relpath(p, ROOT) for p in source_files()], "target": "gfx950",
            "make": " ".join(cmd[:1] + cmd[3:]), "hipcc": hipcc,
+           "from_clean": not incremental, "objects_compiled": compiled, "objects_total": _objects_total(csrc),
+           "linked": linked, "build_seconds": round(time.time() - t0, 1),
            "built_at": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds")}
     with open(RECORD, "w") as f:
         json.dump(rec, f, indent=1)
     return LIB
 
 
+def _objects_total(csrc: str) -> int:
+    r = subprocess.run(["make", "-C", csrc, "-p", "-n", "-q"], capture_output=True, text=True)
+    for ln in (r.stdout or "").splitlines():
+        if ln.startswith("SRCS = ") or ln.startswith("SRCS := "):
+            return len(ln.split("=", 1)[1].split())
+    return -1
+
+
 if __name__ == "__main__":
-    print(build(verbose=True))
+    print(build(verbose=True, incremental="--incremental" in sys.argv))

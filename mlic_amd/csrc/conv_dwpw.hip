@@ -68,7 +68,8 @@ __device__ __forceinline__ int dr_swz(int row) { return (row >> 2) & 3; }
 #ifndef MLIC_DWPW_ROLLED_ALL  // A/B build: 1 = the k-steps of the bias-only form as a loop too
 #define MLIC_DWPW_ROLLED_ALL 0
 #endif
-#ifndef MLIC_DPABL  // diagnostics build: 1 = one MFMA per k-step, 2 = no depthwise math, 4 = no output stores
+#ifndef MLIC_DPABL  // diagnostics build: 1 = one MFMA per k-step, 2 = no depthwise math, 4 = no output stores,
+                    // 16 = the three tap rows all read the centre row (one L1 miss per pixel instead of three)
 #define MLIC_DPABL 0
 #endif
 constexpr int DP_WAVES = 4;
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
       const int yy = y + dy - 1;
       s.vo[dy] = yy >= 0 && yy < H && xl >= 0 && xl < W ? (uint32_t)(yy * W + xl) * 4u + ch : DR_OOB;
     }
+    if (MLIC_DPABL & 16) s.vo[0] = s.vo[2] = s.vo[1];  // diagnostics: every tap row is the centre row (L1 hits)
     return s;
   };
   // one k-step: the lane's 8 channels x 3 rows as pixel pairs (24 dwordx2 loads)

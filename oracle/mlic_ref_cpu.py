@@ -455,10 +455,12 @@ class RefMLIC:
                 "y_hat": y_hat}
 
     @torch.no_grad()
-    def compress_streams(self, x, s: int = 1):
+    def compress_streams(self, x, s: int = 1, likelihoods: bool = False):
         """Encoder side of mlicpp.py:199-290 minus the rANS coder: returns the z symbols
         (round(z - median), int32 [B,C,h,w]) and the 20 per-phase (symbols, indexes) int32
-        arrays in the exact order BufferedRansEncoder receives them, plus y_hat."""
+        arrays in the exact order BufferedRansEncoder receives them, plus y_hat.  likelihoods=True
+        also returns the y / z likelihoods of the same pass (forward's, mlicpp.py:140-185), so
+        bpp_lik comes with the streams at no second network pass."""
         scale = self._vbr_scale(s)
         y = self.g_a(x)
         z = self.h_a(y)
@@ -470,9 +472,12 @@ class RefMLIC:
 
         def record(ph, sym, idx):
             streams[ph] = (sym.clone(), idx.clone())
-        y_hat, _ = self._slice_loop(hyper, y=y, scale=scale, record=record, collect_lik=False)
-        return {"z_symbols": z_sym, "phases": [streams[k] for k in sorted(streams)], "y_hat": y_hat,
-                "z_hat": z_hat}
+        y_hat, y_lik = self._slice_loop(hyper, y=y, scale=scale, record=record, collect_lik=likelihoods)
+        out = {"z_symbols": z_sym, "phases": [streams[k] for k in sorted(streams)], "y_hat": y_hat,
+               "z_hat": z_hat}
+        if likelihoods:
+            out["likelihoods"] = {"y_likelihoods": y_lik, "z_likelihoods": self.eb_likelihood(z)}
+        return out
 
     @torch.no_grad()
     def decode_streams(self, z_symbols, phase_symbols, s: int = 1):

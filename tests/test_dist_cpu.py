@@ -154,3 +154,64 @@ def test_request_streams_cover_the_batch():
     groups = bench.batches(jobs, split=bench.WORKLOADS["vbr-mixed"]["split"])
     assert sorted(len(js) for _, js in groups) == [1, 1, 3, 3]
     assert sorted(j.id for _, js in groups for j in js) == sorted(j.id for j in jobs)
+
+
+def _bench_path_worker(rank, world, port, q):
+    """bench.main()'s distributed skeleton on gloo: the timed region (barriers, device syncs, elapsed
+    max over ranks), the record build for this rank's share of the main config's job list, and the
+    gather with its every-job-exactly-once assert -- the same functions main() calls on RCCL."""
+    import time
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cpu")
+    a = bench.parse(["--config", "main", "--gpus", str(world), "--steps", "2", "--warmup", "0"])
+    jobs, total = bench.build_jobs(a, rank, world)
+    groups = bench.batches(jobs, split=a.split)
+    ran = []
+
+    def run_steps(n):  # rank 1 is the slow one: the reported time must be its time
+        for _ in range(n):
+            for gi, (_, js) in enumerate(groups):
+                ran.append((gi, len(js)))
+            time.sleep(0.05 * (rank + 1))
+    syncs = []
+    elapsed = bench.timed_steps(run_steps, a.steps, True, dev, sync=lambda: syncs.append(1))
+    F = {k: i for i, k in enumerate(mdist.RECORD_FIELDS)}
+    rec = torch.zeros(len(jobs), mdist.RECORD_LEN, dtype=torch.float64)
+    for k, j in enumerate(jobs):
+        rec[k, F["job"]], rec[k, F["H"]], rec[k, F["W"]] = j.id, j.H, j.W
+        rec[k, F["psnr"]] = 20.0 + j.id
+    allrec = bench.gather_all(rec, total, True, dev)
+    # a rank that lost one record: the assert fires on every rank (after the collectives, no hang)
+    lost = None
+    try:
+        bench.gather_all(rec[1:] if rank == 1 else rec, total, True, dev)
+    except AssertionError as e:
+        lost = str(e)
+    q.put((rank, elapsed, len(syncs), len(ran), total, allrec.tolist() if rank == 0 else None, lost))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_distributed_path_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_path_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=180) for _ in range(world)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    el = [g[1] for g in got]
+    assert el[0] == el[1] and el[0] >= 2 * 0.1, el  # max over ranks: the slow rank's 2 x 0.1 s
+    assert all(g[2] == 4 for g in got)  # device sync twice on each side of the timed steps
+    assert all(g[3] == 2 * 4 for g in got)  # 2 steps x the 4 request streams of 8
+    assert all(g[4] == 64 for g in got)
+    rows = got[0][5]
+    assert [int(r[0]) for r in rows] == list(range(64))
+    assert all(abs(r[8] - (20.0 + r[0])) < 1e-9 for r in rows)
+    assert all(g[6] is not None for g in got)  # a lost record is caught on both ranks

@@ -790,3 +790,50 @@ def test_synthesis_fp16_gate(name, rate, H, W):
     PARITY[f"synth_fp16_{name}_{H}x{W}"] = rec
     assert abs(p16 - p32) <= 0.01, rec
     assert rms <= 8.5e-4, rec
+
+
+INTEROP = [("forward_MLICPP_L_192x256_r0", "MLICPP_L", 0, None, 3), ("forward_MLICPP_L_192x256_r2", "MLICPP_L", 2, None, 3),
+           ("forward_MLICPP_L_192x256_r5", "MLICPP_L", 5, None, 3), ("forward_MLICPP_S_192x256_r1", "MLICPP_S", 1, None, 3),
+           ("forward_MLICPP_M_SMALL_DEC_192x256_r1", "MLICPP_M_SMALL_DEC", 1, None, 3),
+           ("forward_MLICPP_M_SMALL_DEC_VBR_192x256_s2_r1", "MLICPP_M_SMALL_DEC_VBR", 1, 2, 3),
+           ("forward_MLICPP_L_128x192", "MLICPP_L", None, None, 0), ("forward_MLICPP_S_128x128", "MLICPP_S", None, None, 0),
+           ("forward_MLICPP_M_SMALL_DEC_128x128", "MLICPP_M_SMALL_DEC", None, None, 0),
+           ("forward_MLICPP_S_VBR_192x256_s1", "MLICPP_S_VBR", None, 1, 3)]
+
+
+@pytest.mark.parametrize("fixture,name,rate,s,img", INTEROP)
+def test_reference_coder_lists_decode(golden, fixture, name, rate, s, img):
+    """Interop: y / z streams built by the native coder from the REFERENCE's own coder
+    lists (the y_symbols / y_indexes / z_symbols its compress() hands BufferedRansEncoder, mlicpp.py:279-281;
+    EntropyBottleneck.compress for z) are what decompress() reads.  Where this codec's scale indexes equal
+    the reference's, the streams are byte-identical to compress()'s own and decode to forward()'s x_hat bit
+    for bit.  Where an index differs (fp32 summation order flipped a scale-table bucket), the decoder reads
+    that symbol with another CDF and the stream desynchronises from there: recorded, not asserted -- a
+    reference-encoded stream decodes here only when the indexes agree."""
+    g = golden(f"{fixture}.npz")
+    H, W = g["x_hat"].shape[-2:]
+    net = rate_net(name, rate) if rate is not None else net_for(name)
+    net.update()
+    kw = {} if s is None else {"stage": 2, "s": s}
+    x = synthetic.synth_image(H, W, img).to(DEV)
+    gc, eb = net.gaussian_conditional, net.entropy_bottleneck
+    gtab = (gc._quantized_cdf.cpu(), gc._cdf_length.cpu(), gc._offset.cpu())
+    etab = (eb._quantized_cdf.cpu(), eb._cdf_length.cpu(), eb._offset.cpu())
+    zs = g["z_symbols"]
+    zidx = np.broadcast_to(np.arange(zs.shape[1], dtype=np.int32)[:, None, None], zs.shape[1:]).reshape(-1)
+    y_ref = entropy.rans_encode(g["y_symbols"], g["y_indexes"], *gtab)
+    z_ref = entropy.rans_encode(zs.reshape(-1), zidx, *etab)
+    c = net.compress(x, **kw)
+    ys, yi, zq = net.encoded_streams(0)
+    agree = bool(np.array_equal(yi, g["y_indexes"]) and np.array_equal(ys, g["y_symbols"])
+                 and np.array_equal(zq, zs.reshape(-1)))
+    d = net.decompress([[y_ref], [z_ref]], torch.Size([H // 64, W // 64]), **kw)
+    f = net(x, **kw)
+    diff = (d["x_hat"] != f["x_hat"])
+    rec = {"indexes_agree": agree, "y_index_mismatch": int((yi != g["y_indexes"]).sum()),
+           "bytes_equal_own": bool(y_ref == c["strings"][0][0] and z_ref == c["strings"][1][0]),
+           "xhat_pixels_differing": int(diff.sum()), "xhat_n": int(diff.numel())}
+    PARITY[f"interop_{fixture}"] = rec
+    if agree:
+        assert rec["bytes_equal_own"], rec
+        assert torch.equal(d["x_hat"], f["x_hat"]), rec
