@@ -176,6 +176,12 @@ struct QuantParams {
   int64_t lik_bs;
   int32_t* sym;  // squeezed symbols or null
   int32_t* idx;  // squeezed indexes or null
+  // the narrow coder streams that cross PCIe (a scale index is < 64; a symbol almost always fits 16
+  // bits): encoder: written beside sym, a symbol beyond int16 saturates sym16 and sets *ovf (the host
+  // then takes the int32 sym); decoder: phase_indexes writes idx8, phase_dequant reads sym16 when set
+  int16_t* sym16;
+  uint8_t* idx8;
+  int* ovf;
   const float* table;
   int ntable;
   int phase;  // 0 anchor, 1 non-anchor

@@ -718,10 +718,17 @@ __global__ void quant_phase_kernel(QuantParams P) {
   if (P.vbr) q = rintf((y - m) * sc);
   else q = rintf(y - m);
   *yh = P.vbr ? q * rs + m : q + m;
-  if (P.sym) {
+  if (P.sym || P.sym16) {
     const int64_t sq = (int64_t)b * P.C * HW / 2 + ((int64_t)c * P.H + h) * (P.W / 2) + (w >> 1);
-    P.sym[sq] = (int32_t)q;
-    P.idx[sq] = scale_index(P.vbr ? s * sc : s, P.table, P.ntable);
+    const int ix = scale_index(P.vbr ? s * sc : s, P.table, P.ntable);
+    if (P.sym) P.sym[sq] = (int32_t)q;
+    if (P.idx) P.idx[sq] = ix;
+    if (P.sym16) {
+      const bool fits = q >= -32768.0f && q <= 32767.0f;
+      P.sym16[sq] = (int16_t)(fits ? q : (q < 0.0f ? -32768.0f : 32767.0f));
+      P.idx8[sq] = (uint8_t)ix;
+      if (!fits) *P.ovf = 1;  // a vector store from the lanes that overflow (benign race: all store 1)
+    }
   }
 }
 
@@ -743,7 +750,10 @@ __global__ void phase_indexes_kernel(QuantParams P) {
   const int h = r / W2, j = r % W2;
   const int w = 2 * j + ((P.phase == 0) ? (1 - (h & 1)) : (h & 1));
   const float s = P.params[(int64_t)b * P.params_bs + (int64_t)c * HW + h * P.W + w];
-  P.idx[(int64_t)b * P.C * P.H * W2 + i] = scale_index(P.vbr ? s * P.sc[b] : s, P.table, P.ntable);
+  const int ix = scale_index(P.vbr ? s * P.sc[b] : s, P.table, P.ntable);
+  const int64_t o = (int64_t)b * P.C * P.H * W2 + i;
+  if (P.idx8) P.idx8[o] = (uint8_t)ix;
+  else P.idx[o] = ix;
 }
 
 void phase_indexes(const QuantParams& P, hipStream_t st) {
@@ -767,7 +777,7 @@ __global__ void phase_dequant_kernel(QuantParams P) {
     return;
   }
   const int64_t sq = (int64_t)b * P.C * HW / 2 + ((int64_t)c * P.H + h) * (P.W / 2) + (w >> 1);
-  const float q = (float)P.sym[sq];
+  const float q = P.sym16 ? (float)P.sym16[sq] : (float)P.sym[sq];
   const float m = P.params[(int64_t)b * P.params_bs + (int64_t)(c + P.C) * HW + p];
   *yh = P.vbr ? q * P.rs[b] + m : q + m;
 }

@@ -470,10 +470,8 @@ Model::~Model() {
 
 Lane::~Lane() {
   if (rflag) (void)hipFree(rflag);
-  if (h_sym) (void)hipHostFree(h_sym);
-  if (h_idx) (void)hipHostFree(h_idx);
-  if (hc_sym) (void)hipHostFree(hc_sym);
-  if (hc_idx) (void)hipHostFree(hc_idx);
+  for (void* p : {(void*)h_sym, (void*)h_sym16, (void*)h_idx8, (void*)hc_sym, (void*)hc_sym16, (void*)hc_idx8})
+    if (p) (void)hipHostFree(p);
   if (cev) (void)hipEventDestroy(cev);
   if (cst) (void)hipStreamDestroy(cst);
   for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
@@ -1164,45 +1162,63 @@ class PhaseDecoder {
  public:
   // single: y[0] holds every image's symbols, phase-major then image-minor (the reference's batched
   // stream); one decoder then walks the images of each phase in order
-  PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym, int32_t* h_idx,
-               HostStats* hs, HostPool* pool, bool single = false)
-      : t_(t), h_sym_(h_sym), h_idx_(h_idx), hs_(hs), pool_(pool), B_(B) {
+  PhaseDecoder(int B, const uint8_t* const* y, const size_t* ylen, const CdfTables* t, int32_t* h_sym,
+               int16_t* h_sym16, uint8_t* h_idx8, HostStats* hs, HostPool* pool, bool single = false)
+      : t_(t), h_sym_(h_sym), h_sym16_(h_sym16), h_idx8_(h_idx8), hs_(hs), pool_(pool), B_(B) {
     dec_.resize(single ? 1 : B);
     for (size_t b = 0; b < dec_.size(); ++b) dec_[b].set_stream(y[b], ylen[b]);
   }
-  void run(int64_t n_per, hipStream_t st, int32_t* d_idx, int32_t* d_sym) {
+  // one phase: uint8 indexes D2H, host rANS decode, symbols H2D as int16 -- or as int32 when one of
+  // the phase's symbols does not fit (returns false: cb->sym then holds them, not cb->sym16)
+  bool run(int64_t n_per, hipStream_t st, const CoderBufs& cb) {
     const int B = B_;
-    HIP_OK(hipMemcpyAsync(h_idx_, d_idx, sizeof(int32_t) * n_per * B, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h_idx8_, cb.idx8, (size_t)n_per * B, hipMemcpyDeviceToHost, st));
     {
       HostStats::Scope w{hs_->wait_ns};
       HIP_OK(hipStreamSynchronize(st));
     }
-    if ((int)dec_.size() == 1 && B > 1) {
+    const int parts = ((int)dec_.size() == 1 && B > 1) ? 1 : B;  // one batched stream: [B][n_per] in order
+    const int64_t n = parts == 1 ? n_per * B : n_per;
+    std::vector<char> wide(parts, 0);
+    auto work = [&](int b) {
       HostStats::Scope d{hs_->dec_ns};
-      dec_[0].decode(h_idx_, n_per * B, *t_, h_sym_);  // [B][n_per] of this phase = the stream's order
+      RansDecoderState& dec = dec_[b];
+      const RansDecoderState::Mark m = dec.mark();
+      if (!dec.decode(h_idx8_ + b * n, n, *t_, h_sym16_ + b * n)) {
+        dec.reset(m);
+        dec.decode(h_idx8_ + b * n, n, *t_, h_sym_ + b * n);
+        wide[b] = 1;
+      }
+    };
+    if (parts == 1) work(0);
+    else pool_->run(B, work, HostPool::DECODE);
+    bool narrow = true;
+    for (char w : wide) narrow = narrow && !w;
+    if (!narrow) {  // widen the parts that fit int16 beside the ones decoded as int32
+      for (int b = 0; b < parts; ++b)
+        if (!wide[b])
+          for (int64_t i = 0; i < n; ++i) h_sym_[b * n + i] = h_sym16_[b * n + i];
+      HIP_OK(hipMemcpyAsync(cb.sym, h_sym_, sizeof(int32_t) * n_per * B, hipMemcpyHostToDevice, st));
     } else {
-      auto work = [&](int b) {
-        HostStats::Scope d{hs_->dec_ns};
-        dec_[b].decode(h_idx_ + b * n_per, n_per, *t_, h_sym_ + b * n_per);
-      };
-      pool_->run(B, work, HostPool::DECODE);
+      HIP_OK(hipMemcpyAsync(cb.sym16, h_sym16_, sizeof(int16_t) * n_per * B, hipMemcpyHostToDevice, st));
     }
-    HIP_OK(hipMemcpyAsync(d_sym, h_sym_, sizeof(int32_t) * n_per * B, hipMemcpyHostToDevice, st));
+    return narrow;
   }
 
  private:
   std::vector<RansDecoderState> dec_;
   const CdfTables* t_;
   int32_t* h_sym_;
-  int32_t* h_idx_;
+  int16_t* h_sym16_;
+  uint8_t* h_idx8_;
   HostStats* hs_;
   HostPool* pool_;
   int B_;
 };
 
 // mlicpp.py:107-176 (forward), 220-277 (compress), 309-366 (decompress)
-void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, int32_t* d_sym,
-                       int32_t* d_idx, PhaseDecoder* dec) {
+void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, const CoderBufs* cb,
+                       PhaseDecoder* dec) {
   const int S = cfg_.S, C = cfg_.C, hM = cfg_.hM();
   const int H = hyper.H, W = hyper.W, HW = H * W;
   const int64_t n_per = (int64_t)C * H * (W / 2);
@@ -1262,13 +1278,11 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       Q.params_bs = par.bs;
       const int phase_id = 2 * idx + ph;
       if (mode == Mode::Decode) {
-        int32_t* di = d_idx;
-        int32_t* ds = d_sym;
-        Q.idx = di;
-        Q.sym = ds;
+        Q.idx8 = cb->idx8;
+        Q.sym = cb->sym;
         if (!L().dry) {
           phase_indexes(Q, L().st);
-          dec->run(n_per, L().st, di, ds);
+          Q.sym16 = dec->run(n_per, L().st, *cb) ? cb->sym16 : nullptr;
           phase_dequant(Q, L().st);
         }
       } else {
@@ -1281,8 +1295,11 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.params_a_bs = pa.bs;
         }
         if (mode == Mode::Encode) {
-          Q.sym = d_sym + (int64_t)phase_id * L().B * n_per;
-          Q.idx = d_idx + (int64_t)phase_id * L().B * n_per;
+          const int64_t off = (int64_t)phase_id * L().B * n_per;
+          Q.sym = cb->sym + off;
+          Q.sym16 = cb->sym16 + off;
+          Q.idx8 = cb->idx8 + off;
+          Q.ovf = cb->ovf;
         }
         timed(PCAT_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); }, "quant_phase");
         Lane& l = L();
@@ -1290,15 +1307,15 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           // this phase's coder inputs leave now: on the lane's copy stream (mode 1), or in the lane's
           // own stream order (mode 2: no extra stream -- streams beyond the box's hardware queues
           // share them, and a queued wait would hold another lane's kernels)
-          const int64_t off = (int64_t)phase_id * l.B * n_per, nb = sizeof(int32_t) * l.B * n_per;
+          const int64_t off = (int64_t)phase_id * l.B * n_per, nb = l.B * n_per;
           hipStream_t cs = l.st;
           if (phase_d2h_mode() == 1) {
             HIP_OK(hipEventRecord(l.cev, l.st));
             HIP_OK(hipStreamWaitEvent(l.cst, l.cev, 0));
             cs = l.cst;
           }
-          HIP_OK(hipMemcpyAsync(l.hc_sym + off, Q.sym, nb, hipMemcpyDeviceToHost, cs));
-          HIP_OK(hipMemcpyAsync(l.hc_idx + off, Q.idx, nb, hipMemcpyDeviceToHost, cs));
+          HIP_OK(hipMemcpyAsync(l.hc_sym16 + off, Q.sym16, sizeof(int16_t) * nb, hipMemcpyDeviceToHost, cs));
+          HIP_OK(hipMemcpyAsync(l.hc_idx8 + off, Q.idx8, nb, hipMemcpyDeviceToHost, cs));
         }
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
@@ -1351,11 +1368,14 @@ void Model::planned(int B, hipStream_t st, F&& body) {
 void Model::ensure_host(size_t n) {
   Lane& l = L();
   if (n <= l.h_cap) return;
-  if (l.h_sym) HIP_OK(hipHostFree(l.h_sym));
-  if (l.h_idx) HIP_OK(hipHostFree(l.h_idx));
-  l.h_sym = l.h_idx = nullptr;
+  for (void* p : {(void*)l.h_sym, (void*)l.h_sym16, (void*)l.h_idx8})
+    if (p) HIP_OK(hipHostFree(p));
+  l.h_sym = nullptr;
+  l.h_sym16 = nullptr;
+  l.h_idx8 = nullptr;
   HIP_OK(hipHostMalloc(&l.h_sym, n * sizeof(int32_t)));
-  HIP_OK(hipHostMalloc(&l.h_idx, n * sizeof(int32_t)));
+  HIP_OK(hipHostMalloc(&l.h_sym16, n * sizeof(int16_t)));
+  HIP_OK(hipHostMalloc(&l.h_idx8, n));
   l.h_cap = n;
 }
 
@@ -1380,11 +1400,14 @@ void Model::ensure_chost(size_t n) {
     HIP_OK(hipEventCreateWithFlags(&l.cev, hipEventDisableTiming));
   }
   if (n <= l.hc_cap) return;
-  if (l.hc_sym) HIP_OK(hipHostFree(l.hc_sym));
-  if (l.hc_idx) HIP_OK(hipHostFree(l.hc_idx));
-  l.hc_sym = l.hc_idx = nullptr;
+  for (void* p : {(void*)l.hc_sym, (void*)l.hc_sym16, (void*)l.hc_idx8})
+    if (p) HIP_OK(hipHostFree(p));
+  l.hc_sym = nullptr;
+  l.hc_sym16 = nullptr;
+  l.hc_idx8 = nullptr;
   HIP_OK(hipHostMalloc(&l.hc_sym, n * sizeof(int32_t)));
-  HIP_OK(hipHostMalloc(&l.hc_idx, n * sizeof(int32_t)));
+  HIP_OK(hipHostMalloc(&l.hc_sym16, n * sizeof(int16_t)));
+  HIP_OK(hipHostMalloc(&l.hc_idx8, n));
   l.hc_cap = n;
 }
 
@@ -1564,7 +1587,7 @@ void Model::forward(const float* x, int B, int H, int W, float* x_hat, float* y_
     eb(z, zh, z_lik, nullptr);
     View hyper = h_s(zh);
     yhat = alloc(cfg_.M, y.H, y.W);
-    slice_loop(Mode::Forward, hyper, &y, yhat, y_lik, nullptr, nullptr, nullptr);
+    slice_loop(Mode::Forward, hyper, &y, yhat, y_lik, nullptr, nullptr);
     // the same policy as compress / decompress: an overflow in the entropy model (g_a .. slice loop)
     // re-runs the whole call in exact fp32 (compress refuses such an input); one in g_s alone re-runs
     // g_s alone, as decompress does, so decompress(compress(x)) == forward(x) bit for bit
@@ -1640,7 +1663,8 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   const int64_t n_per = (int64_t)cfg_.C * h * (w / 2);
   const int nph = 2 * cfg_.S;
   const int64_t ny = (int64_t)nph * B * n_per, nz = (int64_t)B * cfg_.N * hz * wz;
-  int32_t *d_sym = nullptr, *d_idx = nullptr, *d_zsym = nullptr;
+  int32_t* d_zsym = nullptr;
+  CoderBufs cb;
   double* d_bits = nullptr;  // [2][B]: -log2 likelihood sums of y and z per image (B1, rd_loss.py:42-45)
   range_clear(l);
   ensure_chost((size_t)(ny + nz));
@@ -1650,8 +1674,11 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     ~Off() { l.phase_d2h = false; }
   } phase_off{l};
   planned(B, nullptr, [&] {
-    d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
-    d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
+    cb.sym = reinterpret_cast<int32_t*>(l.arena.alloc(ny));
+    cb.sym16 = reinterpret_cast<int16_t*>(l.arena.alloc((ny + 1) / 2));
+    cb.idx8 = reinterpret_cast<uint8_t*>(l.arena.alloc((ny + 3) / 4));
+    cb.ovf = reinterpret_cast<int*>(l.arena.alloc(1));
+    if (!l.dry) HIP_OK(hipMemsetAsync(cb.ovf, 0, sizeof(int), l.st));
     d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(nz));
     d_bits = reinterpret_cast<double*>(l.arena.alloc(4 * B));
     double* part = reinterpret_cast<double*>(l.arena.alloc(4 * neglog2_partial_doubles(B)));
@@ -1665,7 +1692,7 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     eb(z, zh, z_lik, d_zsym);  // z_hat = round(z - med) + med == decompress(compress(z))
     View hyper = h_s(zh);
     View yhat = alloc(cfg_.M, y.H, y.W);
-    slice_loop(Mode::Encode, hyper, &y, yhat, y_lik, d_sym, d_idx, nullptr);
+    slice_loop(Mode::Encode, hyper, &y, yhat, y_lik, &cb, nullptr);
     timed(PCAT_ELEM, 0.0, 4.0 * B * (ny_img + nz_img), [&] {
       neglog2_sum(y_lik, ny_img, B, d_bits, part, l.st);
       neglog2_sum(z_lik, nz_img, B, d_bits + B, part + neglog2_partial_doubles(B), l.st);
@@ -1673,18 +1700,24 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
   });
   std::vector<double> bits(2 * B);
   HIP_OK(hipMemcpyAsync(bits.data(), d_bits, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, l.st));
-  const int32_t* hs = l.hc_sym;
-  const int32_t* hi = l.hc_idx;
   int32_t* hzs = l.hc_sym + ny;
+  // the coder inputs cross PCIe narrow: int16 symbols + uint8 scale indexes (3 B instead of 8 per
+  // symbol); a symbol beyond int16 (set *ovf) brings the int32 copy instead
+  int ovf = 0;
   if (phase_d2h_mode() == 0) {  // every phase in one copy after the network
-    HIP_OK(hipMemcpyAsync(l.hc_sym, d_sym, ny * 4, hipMemcpyDeviceToHost, l.st));
-    HIP_OK(hipMemcpyAsync(l.hc_idx, d_idx, ny * 4, hipMemcpyDeviceToHost, l.st));
+    HIP_OK(hipMemcpyAsync(l.hc_sym16, cb.sym16, ny * sizeof(int16_t), hipMemcpyDeviceToHost, l.st));
+    HIP_OK(hipMemcpyAsync(l.hc_idx8, cb.idx8, ny, hipMemcpyDeviceToHost, l.st));
   }
   HIP_OK(hipMemcpyAsync(hzs, d_zsym, nz * 4, hipMemcpyDeviceToHost, l.st));
+  HIP_OK(hipMemcpyAsync(&ovf, cb.ovf, sizeof(int), hipMemcpyDeviceToHost, l.st));
   {
     HostStats::Scope w{hstats_.wait_ns};
     HIP_OK(hipStreamSynchronize(l.st));
     if (phase_d2h_mode() == 1) HIP_OK(hipStreamSynchronize(l.cst));
+    if (ovf) {
+      HIP_OK(hipMemcpyAsync(l.hc_sym, cb.sym, ny * 4, hipMemcpyDeviceToHost, l.st));
+      HIP_OK(hipStreamSynchronize(l.st));
+    }
   }
   if (prec() != PREC_F32 && range_hit(l)) throw Error(kRangeMsg);
   l.enc.assign(B, EncodedImage{});
@@ -1697,9 +1730,10 @@ void Model::compress_lane(const float* x, int B, int H, int W) {
     HostStats::Scope e{hstats_.enc_ns};
     // y: phases in order, this image's part of each ([phase][B][n_per] in the pinned buffers), coded
     // straight from there: rANS codes LIFO, so the last phase goes in first
-    CoderView v{hs + b * n_per, hi + b * n_per, n_per, (int64_t)B * n_per, nph};
+    CoderView v{ovf ? l.hc_sym + b * n_per : nullptr, ovf ? nullptr : l.hc_sym16 + b * n_per, l.hc_idx8 + b * n_per,
+                n_per, (int64_t)B * n_per, nph};
     RansEncoder enc(v.size());
-    for (int k = nph; k-- > 0;) enc.put_reverse(v.sym + k * v.stride, v.idx + k * v.stride, n_per, gc_);
+    for (int k = nph; k-- > 0;) v.put_phase(enc, k, gc_);
     l.enc[b].y = enc.flush();
     l.enc[b].y_in = v;
     l.enc[b].z_sym.assign(hzs + b * zper, hzs + (b + 1) * zper);
@@ -1746,8 +1780,7 @@ std::string Model::batch_stream(int first, int count) const {
   RansEncoder enc(v0.size() * count);
   for (int k = v0.nph; k-- > 0;)
     for (int b = first + count; b-- > first;) {
-      const CoderView& v = enc_all_[b].y_in;
-      enc.put_reverse(v.sym + k * v.stride, v.idx + k * v.stride, n_per, gc_);
+      enc_all_[b].y_in.put_phase(enc, k, gc_);
     }
   return enc.flush();
 }
@@ -1771,15 +1804,17 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
       dz.decode(zi.data(), zper, eb_, l.h_sym + b * zper);
     }, HostPool::DECODE);
   }
-  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_idx, &hstats_, &host_pool(), batch_stream);
+  PhaseDecoder dec(B, y, ylen, &gc_, l.h_sym, l.h_sym16, l.h_idx8, &hstats_, &host_pool(), batch_stream);
   const int32_t* hz_sym = l.h_sym;
   range_clear(l);
   View yhat;
   const View out{x_hat, 3, 16 * h, 16 * w, (int64_t)3 * 16 * h * 16 * w};
   planned(B, nullptr, [&] {
     int32_t* d_zsym = reinterpret_cast<int32_t*>(l.arena.alloc(B * zper));
-    int32_t* d_sym = reinterpret_cast<int32_t*>(l.arena.alloc(B * n_per));
-    int32_t* d_idx = reinterpret_cast<int32_t*>(l.arena.alloc(B * n_per));
+    CoderBufs cb;
+    cb.sym = reinterpret_cast<int32_t*>(l.arena.alloc(B * n_per));
+    cb.sym16 = reinterpret_cast<int16_t*>(l.arena.alloc((B * n_per + 1) / 2));
+    cb.idx8 = reinterpret_cast<uint8_t*>(l.arena.alloc((B * n_per + 3) / 4));
     View zh = alloc(cfg_.N, hz, wz);
     if (!l.dry) {
       HIP_OK(hipMemcpyAsync(d_zsym, hz_sym, B * zper * 4, hipMemcpyHostToDevice, l.st));
@@ -1788,7 +1823,7 @@ void Model::decompress_lane(const uint8_t* const* y, const size_t* ylen, const u
     }
     View hyper = h_s(zh);
     yhat = alloc(cfg_.M, h, w);
-    slice_loop(Mode::Decode, hyper, nullptr, yhat, nullptr, d_sym, d_idx, &dec);
+    slice_loop(Mode::Decode, hyper, nullptr, yhat, nullptr, &cb, &dec);
     // the entropy model (h_s + slice loop) must match the encoder's arithmetic: no fallback there
     if (!l.dry && prec() != PREC_F32 && range_hit(l)) throw Error(kRangeMsg);
     g_s(yhat, out);

@@ -89,19 +89,38 @@ struct ProfStat {
 };
 
 // An image's y coder inputs where compress left them: the lane's pinned phase-major buffers
-// ([phase][B][n_per]), valid until the model's next compress()
+// ([phase][B][n_per]), valid until the model's next compress().  Symbols are int16 (sym16) unless one
+// of the call's symbols did not fit (then sym, int32); indexes are uint8.
 struct CoderView {
   const int32_t* sym = nullptr;
-  const int32_t* idx = nullptr;
+  const int16_t* sym16 = nullptr;
+  const uint8_t* idx = nullptr;
   int64_t n_per = 0, stride = 0;  // symbols per phase of one image; distance between phases
   int nph = 0;
   int64_t size() const { return n_per * nph; }
-  void gather(int32_t* s, int32_t* i) const {  // coder order: phases in order
+  void gather(int32_t* s, int32_t* i) const {  // coder order: phases in order, widened to int32
     for (int k = 0; k < nph; ++k) {
-      if (s) std::memcpy(s + k * n_per, sym + k * stride, n_per * 4);
-      if (i) std::memcpy(i + k * n_per, idx + k * stride, n_per * 4);
+      for (int64_t j = 0; j < n_per; ++j) {
+        if (s) s[k * n_per + j] = sym16 ? (int32_t)sym16[k * stride + j] : sym[k * stride + j];
+        if (i) i[k * n_per + j] = (int32_t)idx[k * stride + j];
+      }
     }
   }
+  // rANS-code phase k into e (RansEncoder::put_reverse in the stored widths)
+  template <class E, class T>
+  void put_phase(E& e, int k, const T& tables) const {
+    if (sym16) e.put_reverse(sym16 + k * stride, idx + k * stride, n_per, tables);
+    else e.put_reverse(sym + k * stride, idx + k * stride, n_per, tables);
+  }
+};
+
+// device-side coder buffers of one call: encoder [phase][B][n_per] (sym int32 always, sym16 / idx8 the
+// narrow copies that leave for the host, ovf the int16 overflow flag); decoder [B][n_per] of one phase
+struct CoderBufs {
+  int32_t* sym = nullptr;
+  int16_t* sym16 = nullptr;
+  uint8_t* idx8 = nullptr;
+  int* ovf = nullptr;
 };
 
 struct EncodedImage {
@@ -138,15 +157,17 @@ struct Lane {
   std::vector<float> vbr_host;  // [2][B]: per-image gain, then 1 / gain (uploaded by slice_loop)
   bool vbr_on = false;
   std::vector<EncodedImage> enc;
-  int32_t* h_sym = nullptr;
-  int32_t* h_idx = nullptr;
+  int32_t* h_sym = nullptr;    // decoder: z symbols; a phase's symbols when one does not fit int16
+  int16_t* h_sym16 = nullptr;  // decoder: a phase's symbols (H2D)
+  uint8_t* h_idx8 = nullptr;   // decoder: a phase's scale indexes (D2H)
   size_t h_cap = 0;
   // compress: every phase's symbols / indexes leave for these pinned buffers on the copy stream as
   // soon as the phase is quantised, so only the last phase's copy is left when the network ends
   hipStream_t cst = nullptr;
   hipEvent_t cev = nullptr;
-  int32_t* hc_sym = nullptr;
-  int32_t* hc_idx = nullptr;
+  int32_t* hc_sym = nullptr;    // z symbols; the y symbols when one of them did not fit int16
+  int16_t* hc_sym16 = nullptr;  // y symbols
+  uint8_t* hc_idx8 = nullptr;   // y scale indexes
   size_t hc_cap = 0;
   bool phase_d2h = false;
   // profiling
@@ -316,8 +337,8 @@ class Model {
                           const View* hoisted = nullptr);
   void lrp(const std::vector<View>& ins, const std::string& kind, int i, const View& yh_slice, bool anchor);
   View qkv_branch(const View& x, const std::string& p);
-  void slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, int32_t* d_sym,
-                  int32_t* d_idx, class PhaseDecoder* dec);
+  void slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, const CoderBufs* cb,
+                  class PhaseDecoder* dec);
   void eb(const View& z, const View& z_hat, float* z_lik, int32_t* z_sym);
 
   template <class F>

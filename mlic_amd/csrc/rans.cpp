@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <numeric>
 #include <stdexcept>
 
@@ -83,7 +84,8 @@ void RansEncoder::grow() {  // keep the written tail at the end of a larger buff
   ptr_ = end_ - used;
 }
 
-void RansEncoder::put_reverse(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t) {
+template <class S, class I>
+void RansEncoder::put_reverse(const S* symbols, const I* indexes, int64_t n, const CdfTables& t) {
   if (t.enc.empty()) throw std::runtime_error("rans: tables not prepared");
   // One reverse pass.  compressai pushes, per symbol: the symbol (value clamped to max_value) and,
   // if escaped, the bypass length nb (< 15 for 32-bit values) and nb 4-bit chunks of the raw
@@ -102,10 +104,10 @@ void RansEncoder::put_reverse(const int32_t* symbols, const int32_t* indexes, in
       grow();
       ptr = ptr_;
     }
-    const int32_t ci = indexes[i];
+    const int32_t ci = (int32_t)indexes[i];
     if ((uint32_t)ci >= ntab) throw std::runtime_error("rans: cdf index out of range");
     const int32_t max_value = len[ci] - 2;
-    int32_t value = symbols[i] - off[ci];
+    int32_t value = (int32_t)symbols[i] - off[ci];
     if ((uint32_t)value >= (uint32_t)max_value) {  // value < 0 or value >= max_value
       const uint32_t raw = value < 0 ? (uint32_t)(-2 * (int64_t)value - 1) : (uint32_t)(2 * ((int64_t)value - max_value));
       int32_t nb = 0;
@@ -119,6 +121,10 @@ void RansEncoder::put_reverse(const int32_t* symbols, const int32_t* indexes, in
   ptr_ = ptr;
   x_ = x;
 }
+
+template void RansEncoder::put_reverse<int32_t, int32_t>(const int32_t*, const int32_t*, int64_t, const CdfTables&);
+template void RansEncoder::put_reverse<int16_t, uint8_t>(const int16_t*, const uint8_t*, int64_t, const CdfTables&);
+template void RansEncoder::put_reverse<int32_t, uint8_t>(const int32_t*, const uint8_t*, int64_t, const CdfTables&);
 
 std::string RansEncoder::flush() {
   if ((size_t)(ptr_ - out_.data()) < 2) grow();
@@ -148,7 +154,8 @@ uint32_t RansDecoderState::get_word() {
   return pos_ < words_.size() ? words_[pos_++] : 0u;
 }
 
-void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables& t, int32_t* out) {
+template <class I, class S>
+bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S* out) {
   constexpr uint64_t mask = (1ull << PRECISION) - 1;
   constexpr int SHIFT = PRECISION - CdfTables::LUT_BITS;
   const int32_t* len = t.length.data();
@@ -158,7 +165,7 @@ void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables
   const int stride = t.stride;
   uint64_t state = state_;
   for (int64_t i = 0; i < n; ++i) {
-    const int32_t ci = indexes[i];
+    const int32_t ci = (int32_t)indexes[i];
     if ((uint32_t)ci >= (uint32_t)t.n) throw std::runtime_error("rans: cdf index out of range");
     const uint32_t cum = (uint32_t)(state & mask);
     const uint64_t e = lut[((size_t)ci << CdfTables::LUT_BITS) + (cum >> SHIFT)];
@@ -202,10 +209,19 @@ void RansDecoderState::decode(const int32_t* indexes, int64_t n, const CdfTables
       if (raw & 1) value = -value - 1;
       else value += max_value;
     }
-    out[i] = value + off[ci];
+    const int32_t v = value + off[ci];
+    if (sizeof(S) < sizeof(int32_t) && (v < (int32_t)std::numeric_limits<S>::min() || v > (int32_t)std::numeric_limits<S>::max())) {
+      state_ = state;  // the caller resets to its mark and decodes again into a wider type
+      return false;
+    }
+    out[i] = (S)v;
   }
   state_ = state;
+  return true;
 }
+template bool RansDecoderState::decode<int32_t, int32_t>(const int32_t*, int64_t, const CdfTables&, int32_t*);
+template bool RansDecoderState::decode<uint8_t, int32_t>(const uint8_t*, int64_t, const CdfTables&, int32_t*);
+template bool RansDecoderState::decode<uint8_t, int16_t>(const uint8_t*, int64_t, const CdfTables&, int16_t*);
 
 void CdfTables::prepare() {
   enc.assign((size_t)n * stride, EncSym{~0ull, 1, 0, 0, 0});

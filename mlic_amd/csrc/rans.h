@@ -40,7 +40,10 @@ std::string rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t 
 class RansEncoder {
  public:
   explicit RansEncoder(int64_t n_hint);
-  void put_reverse(const int32_t* symbols, const int32_t* indexes, int64_t n, const CdfTables& t);
+  // S: int32_t / int16_t symbols, I: int32_t / uint8_t table indexes (the narrow forms are what crosses
+  // PCIe: a scale index is < 64, a symbol almost always fits 16 bits)
+  template <class S, class I>
+  void put_reverse(const S* symbols, const I* indexes, int64_t n, const CdfTables& t);
   std::string flush();
 
  private:
@@ -54,8 +57,19 @@ class RansEncoder {
 class RansDecoderState {
  public:
   void set_stream(const uint8_t* data, size_t nbytes);
-  // decodes n symbols with the given table indexes
-  void decode(const int32_t* indexes, int64_t n, const CdfTables& t, int32_t* out);
+  // decodes n symbols with the given table indexes; false (output incomplete, state past it) when a
+  // value does not fit S -- reset() to a mark() taken before and decode again into int32_t
+  template <class I, class S>
+  bool decode(const I* indexes, int64_t n, const CdfTables& t, S* out);
+  struct Mark {
+    size_t pos;
+    uint64_t state;
+  };
+  Mark mark() const { return {pos_, state_}; }
+  void reset(const Mark& m) {
+    pos_ = m.pos;
+    state_ = m.state;
+  }
 
  private:
   std::vector<uint32_t> words_;
