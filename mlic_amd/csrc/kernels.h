@@ -44,6 +44,12 @@ void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 bool dwpw_ok(const ConvParams& P, int cin_pad);
 // the model's choice on top of dwpw_ok: grids where the fused kernel measured faster (per image only)
 bool dwpw_grid_ok(const ConvParams& P);
+// producer / consumer form (conv_dwpw2.hip) for Cin = Cout in {96, 128, 160, 192}, W % 4 == 0, bias / GELU
+// (+ residual); dwpw_forward takes it where it applies when $MLIC_DWPW2=1 (A/B; default off)
+bool dwpw2_ok(const ConvParams& P, int cin_pad);
+void dwpw2_set(int on);  // mlic_set_kernel_option("dwpw2"): -1 = $MLIC_DWPW2 (default off), 0 off, 1 on
+void dwpw2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                   const float* dwb, hipStream_t st);
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st);
 

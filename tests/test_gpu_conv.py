@@ -404,12 +404,30 @@ def test_depthwise_strip_vs_tile(B, Cn, H, W, gelu):
     (1, 96, 3, 2, 1),        # a single pair: both halo pairs out of the image
     (1, 192, 5, 960, 1),     # full-resolution width
     (2, 128, 8, 184, 64),    # Cin 128, ragged last segment (4 pairs)
+    # the producer / consumer form (conv_dwpw2.hip: Cin = Cout in 96..192, W % 4 == 0)
+    (2, 192, 98, 480, 1 | 64),  # several 6 x 32 tiles per workgroup, ragged row block (98 = 16 x 6 + 2)
+    (1, 160, 100, 320, 1),   # N = 160, 5 consumer waves
+    (2, 96, 40, 228, 0),     # N = 96, ragged last column tile (228 = 7 x 32 + 4)
 ])
 def test_dwpw_fused(B, Cn, H, W, epi):
     """Fused depthwise 3x3 + pointwise 1x1 (conv_dwpw.hip) == depthwise kernel then the resident-weight
     pointwise kernel, bit for bit (same depthwise order, same MFMA k order), and within the split-fp16
     tolerance of a float64 torch reference (DepthWiseConv, modules/layers/conv.py:22-32)."""
     _dwpw_case(B, Cn, Cn, H, W, epi)
+
+
+@pytest.mark.parametrize("B,Cn,H,W,epi", [
+    (2, 192, 68, 120, 1 | 64), (3, 192, 20, 96, 64), (2, 192, 98, 480, 1 | 64), (1, 160, 100, 320, 1),
+    (2, 96, 40, 228, 0), (2, 128, 8, 184, 64), (1, 192, 5, 960, 1), (2, 192, 40, 100, 1)])
+def test_dwpw2_fused(B, Cn, H, W, epi):
+    """The row-pipelined producer / consumer form (conv_dwpw2.hip, the A/B arm mlic_set_kernel_option
+    ("dwpw2", 1)): the same bits as depthwise + resident pointwise."""
+    from mlic_amd import _lib
+    _lib.call("mlic_set_kernel_option", b"dwpw2", 1)
+    try:
+        _dwpw_case(B, Cn, Cn, H, W, epi)
+    finally:
+        _lib.call("mlic_set_kernel_option", b"dwpw2", -1)
 
 
 # the latent-resolution dwsep convs with Cin != Cout: the LRP's 224 -> 128 GELU and its 128 -> 32 head
