@@ -461,7 +461,7 @@ static void launch_dwpw(const ConvParams& P, const _Float16* wh, const _Float16*
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                   const float* dwb, hipStream_t st) {
   MLIC_CHECK(dwpw_ok(P, cin_pad) && dww, "dwpw: unsupported shape");
-  if (dwpw2_ok(P, cin_pad)) return dwpw2_forward(P, wh, wl, cin_pad, dww, dwb, st);
+  if (dwb && dwpw2_ok(P, cin_pad)) return dwpw2_forward(P, wh, wl, cin_pad, dww, dwb, st);
   const int ct = (P.Cout + 31) / 32, mode = dw_mode(P), res = (P.epi & EPI_RES) ? 1 : 0;
 #define DR_RUN(CIN, CT, M, R)                                        \
   if (P.Cin == CIN && ct == CT && mode == M && res == R) {           \

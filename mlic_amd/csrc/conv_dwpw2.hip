@@ -61,6 +61,9 @@ constexpr int D2_FG = MLIC_D2_FG;
 #ifndef MLIC_D2_DMA  // A/B build: 1 = raw rows staged by LDS-DMA instead of registers
 #define MLIC_D2_DMA 0
 #endif
+#ifndef MLIC_D2_RESPOS  // residual loads: 2 = unmasked (zero page), 0 = exec-masked (wrong results in some
+#define MLIC_D2_RESPOS 2  // rows on gfx950: tools/gpu/d2diag_run.sh), 1 = masked + scheduling fences (same)
+#endif
 
 // the DMA source of a piece outside the image: every DMA wave-instruction is issued by all 64 lanes
 // (a lane-masked skip of a whole instruction would break the producers' counted vmcnt)
@@ -347,6 +350,9 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw2_kernel(ConvParams P, int R,
       bwl[k] = *reinterpret_cast<const half8*>(pl + 16 * k);
     }
   }
+  // the weights landed once, here: otherwise the compiler keeps their loads "in flight" into the row
+  // loop and its per-k-step vmcnt waits there drain the previous row's stores every row
+  __builtin_amdgcn_s_waitcnt(0);
   d2_barrier();  // taps / bias
   const float unscale = ldexpf(1.0f, -P.wexp);
   const uint32_t aoff = d2_aoff(n, h);
@@ -383,6 +389,9 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw2_kernel(ConvParams P, int R,
         al = nl;
       }
       D2_TS(0);
+#if MLIC_D2_RESPOS == 1
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       // epilogue of output row y (pw_resident's op sequence).  The residual: one coalesced dword per lane
       // and channel (whole 128-byte rows), loaded after the MFMAs (before them, its 16 registers beside
       // the weights, the accumulators and the prefetched fragments spill at the three-wave cap)
@@ -390,9 +399,20 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw2_kernel(ConvParams P, int R,
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         xr[q] = 0.0f;
-        if constexpr (RES)
+        if constexpr (RES) {
+#if MLIC_D2_RESPOS == 2
+          const bool rok = y < H && col_ok;
+          xr[q] = *(rok ? rb + (int64_t)(8 * (q >> 2) + 4 * h + (q & 3)) * HW + (int64_t)y * W : d2_zeros);
+#elif MLIC_D2_RESPOS == 3
+          (void)rb;
+#else
           if (y < H && col_ok) xr[q] = rb[(int64_t)(8 * (q >> 2) + 4 * h + (q & 3)) * HW + (int64_t)y * W];
+#endif
+        }
       }
+#if MLIC_D2_RESPOS == 1
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       if (y < H) {
         float* orow = ob + (int64_t)y * W;
 #pragma unroll
@@ -440,21 +460,18 @@ static int d2_mode(const ConvParams& P) {
 // off until it measures faster than dwpw_kernel, profiles/r05/ab/dwpw2_*.log)
 static int g_dwpw2 = -1;
 void dwpw2_set(int on) { g_dwpw2 = on; }
-static bool d2_enabled() {
-  static const bool env = [] {
+// the form chosen: 0 = dwpw_kernel, 1 = dwpw2_kernel, 2 = dwpw3_kernel (conv_dwpw3.hip)
+static int d2_form() {
+  static const int env = [] {
     const char* e = std::getenv("MLIC_DWPW2");
-    return e && std::atoi(e) != 0;
+    return e ? std::atoi(e) : 0;
   }();
-  return g_dwpw2 < 0 ? env : g_dwpw2 != 0;
+  return g_dwpw2 < 0 ? env : g_dwpw2;
 }
-
-// rows per strip: about 32, evened out over the image height
-static int d2_rows(int H) {
-  const int n = std::max(1, (H + 16) / 32);
-  return (H + n - 1) / n;
-}
+static bool d2_enabled() { return d2_form() == 1; }
 
 bool dwpw2_ok(const ConvParams& P, int cin_pad) {
+  if (d2_form() == 2) return dwpw3_shape_ok(P, cin_pad);
   if (!d2_enabled()) return false;
   if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.Cin != P.Cout || (P.Cin != 96 && P.Cin != 128 && P.Cin != 160 && P.Cin != 192)) return false;
@@ -477,6 +494,7 @@ static void launch_dwpw2(const ConvParams& P, const _Float16* wh, const _Float16
 
 void dwpw2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                    const float* dwb, hipStream_t st) {
+  if (d2_form() == 2) return dwpw3_forward(P, wh, wl, cin_pad, dww, dwb, st);
   MLIC_CHECK(dwpw2_ok(P, cin_pad) && dww, "dwpw2: unsupported shape");
   const int mode = d2_mode(P), res = (P.epi & EPI_RES) ? 1 : 0;
 #define D2_RUN(NN)                                                                               \

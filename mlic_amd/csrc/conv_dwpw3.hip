@@ -1,0 +1,402 @@
+// Fused depthwise-separable conv, register-row producer / consumer form ("dwpw3"): the fork's
+// DepthWiseConv (modules/layers/conv.py:22-32, 46-63: depthwise 3x3 stride 1 pad 1 + bias, pointwise
+// 1x1 + bias, then the block's GELU / residual; res_blk.py:62-154) in one kernel for the full-resolution
+// g_a / g_s layers (Cin = Cout = N).  Bit for bit the arithmetic of dwpw_kernel / dwpw2_kernel: the
+// depthwise in dw3x3's FMA order (acc = 0, taps row-major, + bias), the hi / lo split, the three
+// split-fp16 MFMA terms per k-step in pw_resident's order, pw_resident's epilogue.
+//
+// dwpw2 (conv_dwpw2.hip) staged every input row in LDS and read it back three times per output, with the
+// taps, from LDS: its producers issued ~6 LDS reads per channel and pixel and waited on each group of
+// them, and the consumers sat at the barriers (tools/gpu/dwpw2_probe.hip).  Here a producer lane owns one
+// PIXEL column of a 64-pixel strip and its 32 channels live in registers:
+//   * the input row of each channel is one coalesced 256-byte dword load per wave (C), its horizontal
+//     neighbours come from the lanes beside it by DPP wave shifts, and the two strip-edge pixels ride in
+//     a second load (E) whose lanes 0 / 63 the shifts fall back to;
+//   * the vertical window is two running partial sums per channel (pa: the output row two tap rows in,
+//     pb: one tap row in), so each input row is read once and added to the three output rows it touches
+//     in dw3x3's order;
+//   * the taps are wave-uniform: scalar loads (s_load) straight from the weight tensor, FMAs with an SGPR
+//     operand -- no LDS traffic for them;
+//   * the next row's loads are issued channel by channel as soon as the current row's value is consumed,
+//     a whole step of latency ahead.
+// The only LDS traffic is the split depthwise image (two 64-pixel blocks per step, ds_write_b128) and the
+// consumers' MFMA operand reads of it.
+// Consumers (waves 0 .. N/32 - 1): wave w owns output channels 32 w .. 32 w + 31 with its split weights in
+// registers (the A operand of v_mfma_f32_32x32x16_f16 for every k-step), B = the depthwise image; a step is
+// one output row of the strip, two 32-pixel blocks one after the other.  One s_barrier per step: producers
+// write A[(s + 1) & 1] while consumers read A[s & 1].
+// Work unit: a strip of R rows x 64 columns (R ~ 32: 2 rows of vertical halo per R), strips dealt to
+// workgroups in contiguous ranges per XCD.
+// LDS: two A images [k-step][block][hi / lo][32 pixels x 32 bytes] + bias: 97.3 KB at N = 192.
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace mlic {
+
+namespace {
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+constexpr int D3_TC = 64;  // strip width: one pixel per producer lane = two MFMA column blocks
+constexpr int D3_G = 8;    // producer channels per A-image write (one 16-byte piece of hi and of lo)
+
+#ifndef MLIC_D3_TG  // producer channels per scheduling group (2, 4, 8)
+#define MLIC_D3_TG 4
+#endif
+constexpr int D3_TG = MLIC_D3_TG;
+
+// buffer resource over `bytes` bytes at a wave-uniform base (loads past the end return 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t d3_rsrc(const float* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void d3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A image byte offset of pixel row n, channel half g (0: channels 0-7, 1: 8-15) in a 32 x 32-byte block;
+// the 16-byte halves swapped when (n >> 3) & 1 (conflict-free ds_read_b128 for the consumers)
+__device__ __forceinline__ uint32_t d3_aoff(int n, int g) { return (uint32_t)(n * 32 + ((g ^ ((n >> 3) & 1)) << 4)); }
+
+// horizontal neighbours of v (this lane's pixel of one channel): L = lane - 1's (wave_shr:1), R = lane + 1's
+// (wave_shl:1); at the strip edges (lanes 0 / 63, no source lane) the channel's edge pixels, which sit in
+// lanes K / 63 - K of the packed edge register e and are moved into lanes 0 / 63 by row shifts
+template <int K>
+__device__ __forceinline__ void d3_neighbours(float e, float v, float& L, float& R) {
+  const int ei = __builtin_bit_cast(int, e), vi = __builtin_bit_cast(int, v);
+  int el = ei, er = ei;
+  if constexpr (K > 0) {
+    el = __builtin_amdgcn_mov_dpp(ei, 0x100 + K, 0xF, 0xF, true);  // row_shl:K: lane 0 <- lane K
+    er = __builtin_amdgcn_mov_dpp(ei, 0x110 + K, 0xF, 0xF, true);  // row_shr:K: lane 63 <- lane 63 - K
+  }
+  L = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(el, vi, 0x138, 0xF, 0xF, false));
+  R = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(er, vi, 0x130, 0xF, 0xF, false));
+}
+// d3_neighbours for a channel index known after unrolling (the DPP controls are immediates)
+__device__ __forceinline__ void d3_neighbours_k(int k, float e, float v, float& L, float& R) {
+  switch (k) {
+#define D3_NB(K) \
+  case K: return d3_neighbours<K>(e, v, L, R);
+    D3_NB(0) D3_NB(1) D3_NB(2) D3_NB(3) D3_NB(4) D3_NB(5) D3_NB(6) D3_NB(7)
+    D3_NB(8) D3_NB(9) D3_NB(10) D3_NB(11) D3_NB(12) D3_NB(13) D3_NB(14) D3_NB(15)
+#undef D3_NB
+  }
+}
+}  // namespace
+
+// MODE: 0 = bias only, 1 = GELU (dwpw_kernel's modes); RES: residual add last
+template <int N, int MODE, bool RES>
+__global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R, const _Float16* __restrict__ wh,
+                                                           const _Float16* __restrict__ wl, int cin_pad,
+                                                           const float* __restrict__ dww,
+                                                           const float* __restrict__ dwb) {
+  constexpr int NC = N / 32;      // consumer waves (32 output channels each) = producer waves (32 inputs)
+  constexpr int KS = N / 16;      // k-steps of 16 channels
+  constexpr int AB = KS * 4096;   // one A image: [ks][block][hi / lo][1 KB]
+  constexpr int AIMG0 = 0, BIAS0 = 2 * AB;
+  constexpr int LDS = BIAS0 + N * 4;
+  static_assert(LDS <= 160 * 1024, "dwpw3: LDS");
+  __shared__ __attribute__((aligned(16))) char sm[LDS];
+  float* sbias = reinterpret_cast<float*>(sm + BIAS0);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int r = tid; r < N; r += blockDim.x) sbias[r] = P.bias ? P.bias[r] : 0.0f;
+
+  const int H = P.H, W = P.W, HW = H * W;
+  const int nseg = (W + D3_TC - 1) / D3_TC;
+  const int nys = (H + R - 1) / R;
+  const int spi = nseg * nys;  // strips per image, ordered (row band, segment)
+  const int nstrips = spi * P.B;
+  const int xcd = (int)blockIdx.x & 7, nslot = (int)gridDim.x >> 3;
+  const int t_end = (int)((int64_t)(xcd + 1) * nstrips / 8);
+  const int strip0 = (int)((int64_t)xcd * nstrips / 8) + ((int)blockIdx.x >> 3);
+  const int nstrip = strip0 < t_end ? (t_end - strip0 + nslot - 1) / nslot : 0;
+  if (nstrip == 0) return;  // the whole workgroup, before any barrier
+  auto strip_of = [&](int k, int& b, int& ys, int& x0) {
+    const int t = strip0 + k * nslot;
+    b = t / spi;
+    const int r = t - b * spi;
+    const int yb = r / nseg;
+    // (the divisions expand into VALU reciprocals: the results are pinned to scalars, otherwise every
+    // address and row flag derived from them is carried per lane)
+    b = __builtin_amdgcn_readfirstlane(b);
+    ys = __builtin_amdgcn_readfirstlane(yb * R);
+    x0 = __builtin_amdgcn_readfirstlane((r - yb * nseg) * D3_TC);
+  };
+
+  if (wave >= NC) {
+    // ------------------------------------------------------------------------------ producers
+    const int cb = 32 * (wave - NC);  // input channels cb .. cb + 31
+    // this lane's A-image byte offsets (k-step cb / 16, its block and pixel row) for channel halves 0 / 1
+    const uint32_t aw0 = AIMG0 + (uint32_t)(((cb >> 4) * 2 + (lane >> 5)) * 2048) + d3_aoff(lane & 31, 0);
+    const uint32_t aw1 = aw0 - d3_aoff(lane & 31, 0) + d3_aoff(lane & 31, 1);
+    float pa[32], pb[32];  // running sums of output rows Y (two tap rows in) and Y + 1 (one tap row in)
+    // the next input row: sc[j] = channel cb + j at this lane's pixel; the strip-edge pixels of 16 channels
+    // share one register: se[i] lane k < 16 = channel cb + 16 i + k at x0 - 1, lane 63 - k = at x0 + 64
+    float sc[32], se[2];
+    // the strip's input channels cb .. cb + 31 as a buffer resource: a padding pixel (outside the row) is
+    // read at an offset past the end of the buffer, which the hardware returns as 0
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t cxo = 0, exo = 0;  // this lane's pixel / edge pixel byte offsets in a row (or "outside")
+    const uint32_t hw4 = (uint32_t)HW * 4u;
+    // channel j of input row (byte offset so, advanced to channel j + 1) into sc[j], and the edges of
+    // channels j .. j + 15 into se[j / 16] when j % 16 == 15 (so - 15 channels); the offset chain is opaque
+    // to the compiler (it would precompute all 32 channel offsets out of the loops and spill them)
+    auto load_ch = [&](int j, uint32_t& so) {
+      asm volatile("" : "+s"(so));
+      sc[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, cxo, so, 0));
+      if ((j & 15) == 15)
+        se[j >> 4] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, exo, so - 15u * hw4, 0));
+      so += hw4;
+    };
+    // the byte offset of input row Y in the chain (rows outside the image: past the end of the buffer, so
+    // that every load of the row returns 0 -- the padding rows, and the row after a strip's last)
+    auto row_off = [&](int Y) {
+      return (uint32_t)__builtin_amdgcn_readfirstlane(Y >= 0 && Y < H ? Y * W * 4 : 0x40000000);
+    };
+    auto load_row = [&](int Y) {
+      uint32_t so = row_off(Y);
+#pragma unroll
+      for (int j = 0; j < 32; ++j) load_ch(j, so);
+    };
+    // feed the input row held in sc / se: tap row 2 into pa (finishing output row Y, written into A
+    // `buf` when buf >= 0), tap row 1 into pb, tap row 0 starts the next; then load input row `ynext` in
+    // its place (channel by channel: a step of latency ahead).  The same code for every row: in a strip's
+    // first two rows the sums that are not started yet hold stale values and feed only outputs that are
+    // never written (rows above the strip)
+    auto feed = [&](int buf, int ynext) {
+      uint32_t so = row_off(ynext);
+      uint32_t toff = (uint32_t)cb;
+#pragma unroll
+      for (int g = 0; g < 32; g += D3_G) {
+        half8 hv8, lv8;
+#pragma unroll
+        for (int e = 0; e < D3_G; e += 2) {
+          // a scheduling fence per D3_TG channels, and the running channel index of the taps redefined
+          // behind every fence by an opaque (volatile, ordered) statement: the scalar tap loads have no
+          // memory dependences, and without this they float to the top of the row (320 scalar registers
+          // for 32 channels) or out of the row loop altogether
+          if (e % D3_TG == 0) __builtin_amdgcn_sched_barrier(0);
+          asm volatile("" : "+s"(toff));
+          const float* tg = dww + toff * 9;
+          const float* bg = dwb + toff;
+          float o[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            const int j = g + e + f;
+            const float C = sc[j];
+            float L, Rr;
+            d3_neighbours_k(j & 15, se[j >> 4], C, L, Rr);
+            const float* tp = tg + f * 9;
+            float a = pa[j], bs = pb[j], nw = 0.0f;
+            a = fmaf(tp[6], L, a);
+            a = fmaf(tp[7], C, a);
+            a = fmaf(tp[8], Rr, a);
+            bs = fmaf(tp[3], L, bs);
+            bs = fmaf(tp[4], C, bs);
+            bs = fmaf(tp[5], Rr, bs);
+            nw = fmaf(tp[0], L, nw);
+            nw = fmaf(tp[1], C, nw);
+            nw = fmaf(tp[2], Rr, nw);
+            o[f] = a + bg[f];
+            // the channel's results pinned here (opaque, ordered): the arithmetic has no chain of its own
+            // and would otherwise sink to its uses (the A write, the next row) past the fences, keeping
+            // every tap of the group live in scalar registers
+            asm volatile("" : "+v"(o[f]), "+v"(bs), "+v"(nw));
+            pa[j] = bs;
+            pb[j] = nw;
+            load_ch(j, so);
+          }
+          const float2v vv = {o[0], o[1]};
+          const half2v hv = __builtin_convertvector(vv, half2v);
+          const half2v lv = __builtin_convertvector(vv - __builtin_convertvector(hv, float2v), half2v);
+          hv8[e] = hv[0];
+          hv8[e + 1] = hv[1];
+          lv8[e] = lv[0];
+          lv8[e + 1] = lv[1];
+          toff += 2;
+        }
+        if (buf >= 0) {  // (uniform)
+          // k-step cb / 16 + g / 16, channel half (g / 8) & 1 (cb % 32 == 0)
+          char* a = sm + (buf ? AB : 0) + (g >> 4) * 4096 + ((g >> 3) & 1 ? aw1 : aw0);
+          *reinterpret_cast<half8*>(a) = hv8;
+          *reinterpret_cast<half8*>(a + 1024) = lv8;
+        }
+      }
+    };
+    d3_barrier();  // bias written by every wave
+    for (int k = 0; k < nstrip; ++k) {
+      int b, ys, x0;
+      strip_of(k, b, ys, x0);
+      rs = d3_rsrc(P.seg[0].p + (int64_t)b * P.seg[0].bs + (int64_t)cb * HW, 32u * hw4);
+      const int xl = x0 + lane;
+      cxo = xl < W ? (uint32_t)xl * 4u : 0x80000000u;
+      // edge lanes: k < 16 the left edge of channel k, 63 - k the right edge of channel k (+ the load's
+      // first channel); the other lanes read nothing
+      const int xe = lane < 16 ? x0 - 1 : (lane >= 48 ? x0 + D3_TC : -1);
+      const int ek = lane < 16 ? lane : 63 - lane;
+      exo = xe >= 0 && xe < W ? (uint32_t)ek * hw4 + (uint32_t)xe * 4u : 0x80000000u;
+      // input rows ys - 1 + u, u = 0 .. R + 1: row u >= 2 finishes output row ys + u - 2 into A[u & 1]; one
+      // barrier after every u >= 2 (the consumers' strip barrier, then one per output row), plus the one
+      // after the last row's consumption
+      load_row(ys - 1);
+      for (int u = 0; u < R + 3; ++u) {
+        if (u <= R + 1) {
+          // the next row: input row ys + u (none after the strip's last: a padding row)
+          feed(u >= 2 ? (u & 1) : -1, u + 1 <= R + 1 ? ys + u : -1);
+        }
+        if (u >= 2) d3_barrier();
+      }
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------------------------- consumers
+  const int cw = wave;
+  const int n = lane & 31, h = lane >> 5;
+  // weights: A operand of k-step k = W[32 cw .. +32][16 k .. +16]: lane holds row n (output channel
+  // 32 cw + n), channels 16 k + 8 h .. + 8 of hi and of lo; B = the depthwise image (lane: pixel n of the
+  // block, channels 8 h ..), so D = W X: lane = pixel, register q = output channel 32 cw + 8 (q / 4) +
+  // 4 h + q % 4 -- each store instruction writes two whole 128-byte channel rows
+  half8 bwh[KS], bwl[KS];
+  {
+    const _Float16* ph = wh + (int64_t)(32 * cw + n) * cin_pad + 8 * h;
+    const _Float16* pl = wl + (int64_t)(32 * cw + n) * cin_pad + 8 * h;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      bwh[k] = *reinterpret_cast<const half8*>(ph + 16 * k);
+      bwl[k] = *reinterpret_cast<const half8*>(pl + 16 * k);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the weights landed (no weight loads "in flight" inside the row loop)
+  d3_barrier();  // bias
+  const float unscale = ldexpf(1.0f, -P.wexp);
+  const uint32_t aoff = d3_aoff(n, h);
+  const float* sb = sbias + 32 * cw + 4 * h;  // + 8 (q / 4) + q % 4
+  bool bad = false;
+  const uint32_t hw4 = (uint32_t)HW * 4u;
+  for (int k = 0; k < nstrip; ++k) {
+    int b, ys, x0;
+    strip_of(k, b, ys, x0);
+    // the wave's 32 output channels (and residual channels) as buffer resources: a lane outside the image
+    // stores / loads at an offset past the end (dropped / 0) -- no exec-masked memory operations beside
+    // the MFMAs (dwpw2's masked residual loads there gave wrong results in some rows)
+    const auto rs_o = d3_rsrc(P.out + (int64_t)b * P.out_bs + (int64_t)(32 * cw) * HW, 32u * hw4);
+    const auto rs_r = RES ? d3_rsrc(P.res + (int64_t)b * P.res_bs + (int64_t)(32 * cw) * HW, 32u * hw4) : rs_o;
+    d3_barrier();  // the strip's A[0]
+    for (int s = 0; s < R; ++s) {
+      const int y = ys + s;
+#pragma unroll
+      for (int bk = 0; bk < 2; ++bk) {
+        __builtin_amdgcn_sched_barrier(0);  // the two blocks one after the other (one accumulator live)
+        const char* a = sm + AIMG0 + (s & 1) * AB + bk * 2048 + aoff;
+        floatx16 acc;
+        // the B fragments one k-step ahead of their MFMAs
+        half8 ah = *reinterpret_cast<const half8*>(a);
+        half8 al = *reinterpret_cast<const half8*>(a + 1024);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          half8 nh = ah, nl = al;
+          if (ks + 1 < KS) {
+            nh = *reinterpret_cast<const half8*>(a + (ks + 1) * 4096);
+            nl = *reinterpret_cast<const half8*>(a + (ks + 1) * 4096 + 1024);
+          }
+          // pw_resident's term order: (W lo . X hi), (W hi . X lo), (W hi . X hi)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bwl[ks], ah, ks == 0 ? floatx16{} : acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bwh[ks], al, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bwh[ks], ah, acc, 0, 0, 0);
+          ah = nh;
+          al = nl;
+        }
+        // epilogue of output row y, pixel x0 + 32 bk + n (pw_resident's op sequence; residual last).
+        // Register q = output channel 32 cw + 8 (q / 4) + 4 h + q % 4: byte offset vo (pixel, 4 h) + the
+        // uniform channel offset (8 (q / 4) + q % 4) HW 4, a running (opaque) chain
+        const int px = x0 + 32 * bk + n;
+        const bool ok = y < H && px < W;
+        const uint32_t vo = ok ? (uint32_t)(y * W + px) * 4u + (uint32_t)(4 * h) * hw4 : 0x80000000u;
+        uint32_t so = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 b4 = *reinterpret_cast<const float4*>(sb + 8 * g);
+          const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * g + e;
+            asm volatile("" : "+s"(so));
+            float tv = __builtin_fmaf(acc[q], unscale, bq[e]);
+            if constexpr (MODE == 1) tv = gelu_erf(tv);
+            if constexpr (RES) tv = tv + __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_r, vo, so, 0));
+            bad |= ok && !(__builtin_fabsf(tv) <= 3.4e38f);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tv), rs_o, vo, so, 0);
+            so += hw4;
+          }
+          so += 4u * hw4;
+        }
+      }
+      d3_barrier();
+    }
+  }
+  range_report(P.rflag, bad);
+}
+
+static int d3_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return n;
+}
+
+// rows per strip: about 32, evened out over the image height
+static int d3_rows(int H) {
+  const int n = std::max(1, (H + 16) / 32);
+  return (H + n - 1) / n;
+}
+
+bool dwpw3_shape_ok(const ConvParams& P, int cin_pad) {
+  if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
+  if (P.Cin != P.Cout || (P.Cin != 96 && P.Cin != 128 && P.Cin != 160 && P.Cin != 192)) return false;
+  const int e = P.epi & ~EPI_RES;
+  if (e != EPI_NONE && e != EPI_GELU) return false;
+  if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W) return false;
+  if ((int64_t)P.Cin * P.H * P.W * 4 >= (1ll << 31)) return false;
+  return true;
+}
+static bool d3_args_ok(const float* dww, const float* dwb) { return dww && dwb; }  // (the depthwise has a bias)
+
+template <int N, int M, bool RS>
+static void launch_dwpw3(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                         const float* dwb, hipStream_t st) {
+  const int R = d3_rows(P.H);
+  const int64_t want = (int64_t)((P.W + D3_TC - 1) / D3_TC) * ((P.H + R - 1) / R) * P.B;
+  const int64_t g = std::min<int64_t>(want, (int64_t)d3_num_cus());
+  const dim3 grid((unsigned)((g + 7) / 8 * 8));  // a multiple of 8: the XCD-aware deal
+  hipLaunchKernelGGL((dwpw3_kernel<N, M, RS>), grid, dim3(N / 16 * 64), 0, st, P, R, wh, wl, cin_pad, dww, dwb);
+  HIP_OK(hipGetLastError());
+}
+
+void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                   const float* dwb, hipStream_t st) {
+  MLIC_CHECK(dwpw3_shape_ok(P, cin_pad) && d3_args_ok(dww, dwb), "dwpw3: unsupported shape");
+  const int mode = (P.epi & EPI_GELU) ? 1 : 0, res = (P.epi & EPI_RES) ? 1 : 0;
+#define D3_RUN(NN)                                                                               \
+  if (P.Cin == NN) {                                                                             \
+    if (mode == 0 && !res) return launch_dwpw3<NN, 0, false>(P, wh, wl, cin_pad, dww, dwb, st); \
+    if (mode == 0 && res) return launch_dwpw3<NN, 0, true>(P, wh, wl, cin_pad, dww, dwb, st);   \
+    if (mode == 1 && !res) return launch_dwpw3<NN, 1, false>(P, wh, wl, cin_pad, dww, dwb, st); \
+    return launch_dwpw3<NN, 1, true>(P, wh, wl, cin_pad, dww, dwb, st);                          \
+  }
+  D3_RUN(192) D3_RUN(160) D3_RUN(128) D3_RUN(96)
+#undef D3_RUN
+}
+
+}  // namespace mlic

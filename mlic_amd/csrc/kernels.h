@@ -47,7 +47,12 @@ bool dwpw_grid_ok(const ConvParams& P);
 // producer / consumer form (conv_dwpw2.hip) for Cin = Cout in {96, 128, 160, 192}, W % 4 == 0, bias / GELU
 // (+ residual); dwpw_forward takes it where it applies when $MLIC_DWPW2=1 (A/B; default off)
 bool dwpw2_ok(const ConvParams& P, int cin_pad);
-void dwpw2_set(int on);  // mlic_set_kernel_option("dwpw2"): -1 = $MLIC_DWPW2 (default off), 0 off, 1 on
+// mlic_set_kernel_option("dwpw2"): -1 = $MLIC_DWPW2 (default 0), 0 = dwpw_kernel, 1 = the row-pipelined
+// LDS form (conv_dwpw2.hip), 2 = the register-row form (conv_dwpw3.hip)
+void dwpw2_set(int on);
+bool dwpw3_shape_ok(const ConvParams& P, int cin_pad);
+void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                   const float* dwb, hipStream_t st);
 void dwpw2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                    const float* dwb, hipStream_t st);
 void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,

@@ -416,14 +416,18 @@ def test_dwpw_fused(B, Cn, H, W, epi):
     _dwpw_case(B, Cn, Cn, H, W, epi)
 
 
+@pytest.mark.parametrize("form", [1, 2])
 @pytest.mark.parametrize("B,Cn,H,W,epi", [
     (2, 192, 68, 120, 1 | 64), (3, 192, 20, 96, 64), (2, 192, 98, 480, 1 | 64), (1, 160, 100, 320, 1),
-    (2, 96, 40, 228, 0), (2, 128, 8, 184, 64), (1, 192, 5, 960, 1), (2, 192, 40, 100, 1)])
-def test_dwpw2_fused(B, Cn, H, W, epi):
-    """The row-pipelined producer / consumer form (conv_dwpw2.hip, the A/B arm mlic_set_kernel_option
-    ("dwpw2", 1)): the same bits as depthwise + resident pointwise."""
+    (2, 96, 40, 228, 0), (2, 128, 8, 184, 64), (1, 192, 5, 960, 1), (2, 192, 40, 100, 1),
+    (1, 96, 33, 62, 1 | 64), (2, 160, 9, 130, 1), (1, 128, 70, 64, 1 | 64)])
+def test_dwpw2_fused(B, Cn, H, W, epi, form):
+    """The producer / consumer forms (A/B arms of mlic_set_kernel_option("dwpw2", form)): 1 = the
+    row-pipelined LDS form (conv_dwpw2.hip), 2 = the register-row form (conv_dwpw3.hip, 64-pixel strips:
+    ragged, narrower-than-a-strip and exact-multiple widths): the same bits as depthwise + resident
+    pointwise."""
     from mlic_amd import _lib
-    _lib.call("mlic_set_kernel_option", b"dwpw2", 1)
+    _lib.call("mlic_set_kernel_option", b"dwpw2", form)
     try:
         _dwpw_case(B, Cn, Cn, H, W, epi)
     finally:
