@@ -470,6 +470,12 @@ static int d2_form() {
 }
 static bool d2_enabled() { return d2_form() == 1; }
 
+// rows per strip: about 32, evened out over the image height
+static int d2_rows(int H) {
+  const int n = std::max(1, (H + 16) / 32);
+  return (H + n - 1) / n;
+}
+
 bool dwpw2_ok(const ConvParams& P, int cin_pad) {
   if (d2_form() == 2) return dwpw3_shape_ok(P, cin_pad);
   if (!d2_enabled()) return false;
