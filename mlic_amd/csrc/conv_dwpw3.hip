@@ -296,6 +296,21 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
 #pragma unroll
       for (int bk = 0; bk < 2; ++bk) {
         __builtin_amdgcn_sched_barrier(0);  // the two blocks one after the other (one accumulator live)
+        // this lane's output pixel and byte offset (pixel, channel 4 h); the residual of the block is loaded
+        // before its MFMAs (16 dword loads in flight beside them)
+        const int px = x0 + 32 * bk + n;
+        const bool ok = y < H && px < W;
+        const uint32_t vo = ok ? (uint32_t)(y * W + px) * 4u + (uint32_t)(4 * h) * hw4 : 0x80000000u;
+        float xr[16];
+        if constexpr (RES) {
+          uint32_t so = 0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            asm volatile("" : "+s"(so));
+            xr[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_r, vo, so, 0));
+            so += (q & 3) == 3 ? 5u * hw4 : hw4;
+          }
+        }
         const char* a = sm + AIMG0 + (s & 1) * AB + bk * 2048 + aoff;
         floatx16 acc;
         // the B fragments one k-step ahead of their MFMAs
@@ -318,9 +333,6 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
         // epilogue of output row y, pixel x0 + 32 bk + n (pw_resident's op sequence; residual last).
         // Register q = output channel 32 cw + 8 (q / 4) + 4 h + q % 4: byte offset vo (pixel, 4 h) + the
         // uniform channel offset (8 (q / 4) + q % 4) HW 4, a running (opaque) chain
-        const int px = x0 + 32 * bk + n;
-        const bool ok = y < H && px < W;
-        const uint32_t vo = ok ? (uint32_t)(y * W + px) * 4u + (uint32_t)(4 * h) * hw4 : 0x80000000u;
         uint32_t so = 0;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             asm volatile("" : "+s"(so));
             float tv = __builtin_fmaf(acc[q], unscale, bq[e]);
             if constexpr (MODE == 1) tv = gelu_erf(tv);
-            if constexpr (RES) tv = tv + __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_r, vo, so, 0));
+            if constexpr (RES) tv = tv + xr[q];
             bad |= ok && !(__builtin_fabsf(tv) <= 3.4e38f);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tv), rs_o, vo, so, 0);
             so += hw4;
