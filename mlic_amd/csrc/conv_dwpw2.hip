@@ -460,11 +460,13 @@ static int d2_mode(const ConvParams& P) {
 // off until it measures faster than dwpw_kernel, profiles/r05/ab/dwpw2_*.log)
 static int g_dwpw2 = -1;
 void dwpw2_set(int on) { g_dwpw2 = on; }
-// the form chosen: 0 = dwpw_kernel, 1 = dwpw2_kernel, 2 = dwpw3_kernel (conv_dwpw3.hip)
+// the form chosen: 0 = dwpw_kernel, 1 = dwpw2_kernel, 2 = dwpw3_kernel (conv_dwpw3.hip, the default: 8 x 192
+// x 544 x 960 bias / GELU / GELU + residual 1.85 / 2.01 / 2.15 ms against dwpw_kernel's 2.31 / 2.45 / 2.98,
+// profiles/r05/ab/dwpw3_ab.log)
 static int d2_form() {
   static const int env = [] {
     const char* e = std::getenv("MLIC_DWPW2");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 2;
   }();
   return g_dwpw2 < 0 ? env : g_dwpw2;
 }

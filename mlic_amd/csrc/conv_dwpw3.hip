@@ -137,7 +137,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     // this lane's A-image byte offsets (k-step cb / 16, its block and pixel row) for channel halves 0 / 1
     const uint32_t aw0 = AIMG0 + (uint32_t)(((cb >> 4) * 2 + (lane >> 5)) * 2048) + d3_aoff(lane & 31, 0);
     const uint32_t aw1 = aw0 - d3_aoff(lane & 31, 0) + d3_aoff(lane & 31, 1);
-    float pa[32], pb[32];  // running sums of output rows Y (two tap rows in) and Y + 1 (one tap row in)
+    float pa[32], pb[32];  // running sums of two output rows (two / one tap rows in, roles alternating)
     // the next input row: sc[j] = channel cb + j at this lane's pixel; the strip-edge pixels of 16 channels
     // share one register: se[i] lane k < 16 = channel cb + 16 i + k at x0 - 1, lane 63 - k = at x0 + 64
     float sc[32], se[2];
@@ -171,7 +171,9 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     // its place (channel by channel: a step of latency ahead).  The same code for every row: in a strip's
     // first two rows the sums that are not started yet hold stale values and feed only outputs that are
     // never written (rows above the strip)
-    auto feed = [&](int buf, int ynext) {
+    // F: the sums two tap rows in (finished by this row), A: one tap row in.  After the row A holds the
+    // sums two rows in and F the new ones: the caller swaps the roles (no register moves)
+    auto feed = [&](float (&F)[32], float (&A)[32], int buf, int ynext) {
       uint32_t so = row_off(ynext);
       uint32_t toff = (uint32_t)cb;
 #pragma unroll
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             float L, Rr;
             d3_neighbours_k(j & 15, se[j >> 4], C, L, Rr);
             const float* tp = tg + f * 9;
-            float a = pa[j], bs = pb[j], nw = 0.0f;
+            float a = F[j], bs = A[j], nw = 0.0f;
             a = fmaf(tp[6], L, a);
             a = fmaf(tp[7], C, a);
             a = fmaf(tp[8], Rr, a);
@@ -210,8 +212,8 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             // and would otherwise sink to its uses (the A write, the next row) past the fences, keeping
             // every tap of the group live in scalar registers
             asm volatile("" : "+v"(o[f]), "+v"(bs), "+v"(nw));
-            pa[j] = bs;
-            pb[j] = nw;
+            A[j] = bs;
+            F[j] = nw;
             load_ch(j, so);
           }
           const float2v vv = {o[0], o[1]};
@@ -247,12 +249,14 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
       // barrier after every u >= 2 (the consumers' strip barrier, then one per output row), plus the one
       // after the last row's consumption
       load_row(ys - 1);
-      for (int u = 0; u < R + 3; ++u) {
-        if (u <= R + 1) {
-          // the next row: input row ys + u (none after the strip's last: a padding row)
-          feed(u >= 2 ? (u & 1) : -1, u + 1 <= R + 1 ? ys + u : -1);
-        }
+      // the next row of step u: input row ys + u (none after the strip's last: a padding row)
+      auto step = [&](int u, float (&F)[32], float (&A)[32]) {
+        if (u <= R + 1) feed(F, A, u >= 2 ? (u & 1) : -1, u + 1 <= R + 1 ? ys + u : -1);
         if (u >= 2) d3_barrier();
+      };
+      for (int u = 0; u < R + 3; u += 2) {  // two steps per trip: the sum roles alternate
+        step(u, pa, pb);
+        if (u + 1 < R + 3) step(u + 1, pb, pa);
       }
     }
     return;

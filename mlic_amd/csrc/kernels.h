@@ -44,10 +44,10 @@ void conv_smallcin_forward(const ConvParams& P, hipStream_t st);
 bool dwpw_ok(const ConvParams& P, int cin_pad);
 // the model's choice on top of dwpw_ok: grids where the fused kernel measured faster (per image only)
 bool dwpw_grid_ok(const ConvParams& P);
-// producer / consumer form (conv_dwpw2.hip) for Cin = Cout in {96, 128, 160, 192}, W % 4 == 0, bias / GELU
-// (+ residual); dwpw_forward takes it where it applies when $MLIC_DWPW2=1 (A/B; default off)
+// producer / consumer forms for Cin = Cout in {96, 128, 160, 192}, bias / GELU (+ residual): dwpw_forward
+// takes the chosen one (dwpw2_set) where it applies
 bool dwpw2_ok(const ConvParams& P, int cin_pad);
-// mlic_set_kernel_option("dwpw2"): -1 = $MLIC_DWPW2 (default 0), 0 = dwpw_kernel, 1 = the row-pipelined
+// mlic_set_kernel_option("dwpw2"): -1 = $MLIC_DWPW2 (default 2), 0 = dwpw_kernel, 1 = the row-pipelined
 // LDS form (conv_dwpw2.hip), 2 = the register-row form (conv_dwpw3.hip)
 void dwpw2_set(int on);
 bool dwpw3_shape_ok(const ConvParams& P, int cin_pad);
