@@ -44,8 +44,17 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 constexpr int D3_TC = 64;  // strip width: one pixel per producer lane = two MFMA column blocks
 constexpr int D3_G = 8;    // producer channels per A-image write (one 16-byte piece of hi and of lo)
 
+#ifndef MLIC_D3_PK  // consumer epilogue on channel pairs with packed-fp32 VALU (A/B: 0 = scalar)
+#define MLIC_D3_PK 1
+#endif
+#ifndef MLIC_D3_PPK  // producer depthwise on channel pairs with packed-fp32 VALU (A/B: 0 = scalar)
+#define MLIC_D3_PPK 1
+#endif
+#ifndef MLIC_D3_TPF  // producer taps prefetched one channel pair ahead (A/B: 0 = loaded at use)
+#define MLIC_D3_TPF 0
+#endif
 #ifndef MLIC_D3_TG  // producer channels per scheduling group (2, 4, 8)
-#define MLIC_D3_TG 4
+#define MLIC_D3_TG (MLIC_D3_TPF ? 2 : 4)
 #endif
 constexpr int D3_TG = MLIC_D3_TG;
 
@@ -176,6 +185,20 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     auto feed = [&](float (&F)[32], float (&A)[32], int buf, int ynext) {
       uint32_t so = row_off(ynext);
       uint32_t toff = (uint32_t)cb;
+#if MLIC_D3_TPF
+      // taps + bias of the current channel pair in scalar registers, the next pair's loaded one pair ahead
+      // (the last pair of the row prefetches the first: the taps are the same every row)
+      float tcur[20], tnxt[20];
+      auto load_taps = [&](uint32_t t, float (&d)[20]) {
+        const float* tp = dww + t * 9;
+#pragma unroll
+        for (int k = 0; k < 18; ++k) d[k] = tp[k];
+        d[18] = dwb[t];
+        d[19] = dwb[t + 1];
+      };
+      asm volatile("" : "+s"(toff));
+      load_taps(toff, tcur);
+#endif
 #pragma unroll
       for (int g = 0; g < 32; g += D3_G) {
         half8 hv8, lv8;
@@ -186,9 +209,46 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
           // memory dependences, and without this they float to the top of the row (320 scalar registers
           // for 32 channels) or out of the row loop altogether
           if (e % D3_TG == 0) __builtin_amdgcn_sched_barrier(0);
+#if MLIC_D3_TPF
+          uint32_t tnext = (g + e + 2 < 32) ? toff + 2 : (uint32_t)cb;
+          asm volatile("" : "+s"(tnext));
+          load_taps(tnext, tnxt);
+          const float* tg = tcur;
+          const float* bg = tcur + 18;
+#else
           asm volatile("" : "+s"(toff));
           const float* tg = dww + toff * 9;
           const float* bg = dwb + toff;
+#endif
+#if MLIC_D3_PPK
+          // the channel pair (j, j + 1) as packed-fp32 VALU: each v_pk_fma_f32 is the two channels' fma,
+          // element for element the scalar sequence (taps paired into scalar register pairs)
+          const int j = g + e;
+          float Ls[2], Rs[2];
+          d3_neighbours_k(j & 15, se[j >> 4], sc[j], Ls[0], Rs[0]);
+          d3_neighbours_k((j + 1) & 15, se[(j + 1) >> 4], sc[j + 1], Ls[1], Rs[1]);
+          const mlic_float2 L2 = {Ls[0], Ls[1]}, C2 = {sc[j], sc[j + 1]}, R2 = {Rs[0], Rs[1]};
+          auto tap = [&](int k) { return mlic_float2{tg[k], tg[9 + k]}; };
+          mlic_float2 a2 = {F[j], F[j + 1]}, b2 = {A[j], A[j + 1]}, n2 = {0.0f, 0.0f};
+          a2 = __builtin_elementwise_fma(tap(6), L2, a2);
+          a2 = __builtin_elementwise_fma(tap(7), C2, a2);
+          a2 = __builtin_elementwise_fma(tap(8), R2, a2);
+          b2 = __builtin_elementwise_fma(tap(3), L2, b2);
+          b2 = __builtin_elementwise_fma(tap(4), C2, b2);
+          b2 = __builtin_elementwise_fma(tap(5), R2, b2);
+          n2 = __builtin_elementwise_fma(tap(0), L2, n2);
+          n2 = __builtin_elementwise_fma(tap(1), C2, n2);
+          n2 = __builtin_elementwise_fma(tap(2), R2, n2);
+          mlic_float2 o2 = a2 + mlic_float2{bg[0], bg[1]};
+          asm volatile("" : "+v"(o2), "+v"(b2), "+v"(n2));
+          A[j] = b2[0];
+          A[j + 1] = b2[1];
+          F[j] = n2[0];
+          F[j + 1] = n2[1];
+          load_ch(j, so);
+          load_ch(j + 1, so);
+          const float o[2] = {o2[0], o2[1]};
+#else
           float o[2];
 #pragma unroll
           for (int f = 0; f < 2; ++f) {
@@ -216,6 +276,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             F[j] = nw;
             load_ch(j, so);
           }
+#endif
           const float2v vv = {o[0], o[1]};
           const half2v hv = __builtin_convertvector(vv, half2v);
           const half2v lv = __builtin_convertvector(vv - __builtin_convertvector(hv, float2v), half2v);
@@ -224,6 +285,14 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
           lv8[e] = lv[0];
           lv8[e + 1] = lv[1];
           toff += 2;
+#if MLIC_D3_TPF
+          // the next pair's taps must have landed here, a pair of work after their loads (ordered use)
+#pragma unroll
+          for (int k = 0; k < 20; k += 4)
+            asm volatile("" ::"s"(tnxt[k]), "s"(tnxt[k + 1]), "s"(tnxt[k + 2]), "s"(tnxt[k + 3]));
+#pragma unroll
+          for (int k = 0; k < 20; ++k) tcur[k] = tnxt[k];
+#endif
         }
         if (buf >= 0) {  // (uniform)
           // k-step cb / 16 + g / 16, channel half (g / 8) & 1 (cb % 32 == 0)
@@ -342,6 +411,28 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
         for (int g = 0; g < 4; ++g) {
           const float4 b4 = *reinterpret_cast<const float4*>(sb + 8 * g);
           const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#if MLIC_D3_PK
+          // channel pairs: the scale / bias FMA, GELU and residual add as packed-fp32 VALU (gelu_erf2: the
+          // same operations element for element)
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int q = 4 * g + e;
+            mlic_float2 t2 = __builtin_elementwise_fma(mlic_float2{acc[q], acc[q + 1]}, mlic_float2{unscale, unscale},
+                                                       mlic_float2{bq[e], bq[e + 1]});
+            if constexpr (MODE == 1) t2 = gelu_erf2(t2);
+            if constexpr (RES) t2 = t2 + mlic_float2{xr[q], xr[q + 1]};
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              asm volatile("" : "+s"(so));
+              // (the element copied out first: __builtin_bit_cast of the vector element lvalue t2[f] reads
+              // element 0 whatever f is -- seen in the ISA)
+              const float tv = t2[f];
+              bad |= ok && !(__builtin_fabsf(tv) <= 3.4e38f);
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tv), rs_o, vo, so, 0);
+              so += hw4;
+            }
+          }
+#else
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int q = 4 * g + e;
@@ -353,6 +444,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tv), rs_o, vo, so, 0);
             so += hw4;
           }
+#endif
           so += 4u * hw4;
         }
       }

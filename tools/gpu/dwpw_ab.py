@@ -37,7 +37,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     P = C.c_void_p
     outs = {}
-    for epi in (0, 1, 65):
+    epis = [int(e) for e in os.environ.get("DWPW_EPI", "0,1,65").split(",")]  # (one mode for PMC passes)
+    for epi in epis:
         res = P(r.data_ptr()) if epi & 64 else None
         f = lambda: _lib.call("mlic_dwpw_run", P(st), P(x.data_ptr()), P(dw.data_ptr()), P(db.data_ptr()),  # noqa
                               P(w.data_ptr()), P(b.data_ptr()), P(y.data_ptr()), B, Cn, Cn, H, W, epi, res)
