@@ -48,7 +48,7 @@ constexpr int D3_G = 8;    // producer channels per A-image write (one 16-byte p
 #define MLIC_D3_PK 1
 #endif
 #ifndef MLIC_D3_PPK  // producer depthwise on channel pairs with packed-fp32 VALU (A/B: 0 = scalar)
-#define MLIC_D3_PPK 1
+#define MLIC_D3_PPK 0
 #endif
 #ifndef MLIC_D3_TPF  // producer taps prefetched one channel pair ahead (A/B: 0 = loaded at use)
 #define MLIC_D3_TPF 0

@@ -1,16 +1,18 @@
 # Round measurement record.  usage on the box:
 #   bash tools/gpu/record_round.sh <outdir> [kernel-family] [stages]
-# stages (default "tests pmc bench rocprof"):
+# stages (default "tests pmc bench decode rocprof"):
 #   tests    GPU suite (workspace + outputs NaN-poisoned, tests/conftest.py) with exact parity counts
 #   pmc      FETCH_SIZE / WRITE_SIZE of the dominant family over the isolated pass's launches
 #            (one lane, 8 images: bench.py --lanes 1 --batch 8 --split 1), tools/pmc_traffic.py -> traffic.json
 #   bench    the default bench line (roofline.traffic from traffic.json) + per-layer table
+#   decode   the decode-only line (bench.py --phase decode: decompress of streams encoded before the
+#            timed region), same traffic file
 #   rocprof  rocprofv3 --kernel-trace --stats of the isolated pass alone (the launches the line's
 #            roofline.frac divides by) and of the timed configuration alone
 cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/record}
 KERN=${2:-conv_x4_kernel}
-STAGES=${3:-"tests pmc bench rocprof"}
+STAGES=${3:-"tests pmc bench decode rocprof"}
 ISO="--lanes 1 --batch 8 --split 1"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -41,6 +43,12 @@ if has bench; then
   timeout -k 10 600 python3 -u bench.py --traffic-json "$TJ" --layers-out "$OUT/layers.tsv" \
     > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed $?"; tail -30 "$OUT/bench.err"; exit 1; }
   head -c 400 "$OUT/bench.json"; echo
+fi
+if has decode; then
+  TJ="$OUT/traffic.json"; [ -f "$TJ" ] || TJ=profiles/traffic_r04.json
+  timeout -k 10 600 python3 -u bench.py --phase decode --traffic-json "$TJ" > "$OUT/bench_decode.json" \
+    2> "$OUT/bench_decode.err" || { echo "bench decode failed $?"; tail -30 "$OUT/bench_decode.err"; exit 1; }
+  head -c 300 "$OUT/bench_decode.json"; echo
 fi
 if has rocprof; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_iso" -o run -- \
