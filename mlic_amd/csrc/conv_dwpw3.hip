@@ -464,10 +464,23 @@ static int d3_num_cus() {
   return n;
 }
 
-// rows per strip: about 32, evened out over the image height
-static int d3_rows(int H) {
-  const int n = std::max(1, (H + 16) / 32);
-  return (H + n - 1) / n;
+// rows per strip: the R in 8 .. 34 with the fewest steps for the busiest workgroup, rounds of strips over
+// the CUs x (R + 2 halo rows + ~1 step of strip overhead).  544 x 960 x 8 keeps R = 32 (2040 strips,
+// 8 rounds); 272 x 480 x 8 takes R = 34 (512 strips: 2 rounds of 37 steps, against 3 of 35 at R = 32) and
+// 136 x 240 x 8 R = 17 (256 strips: every CU busy, against 128 at R = 34)
+static int d3_rows(int B, int H, int W) {
+  const int64_t ncu = d3_num_cus(), nseg = (W + D3_TC - 1) / D3_TC;
+  int best = std::min(H, 32);
+  int64_t best_cost = INT64_MAX;
+  for (int R = std::min(H, 34); R >= std::min(H, 8); --R) {
+    const int64_t strips = (int64_t)B * nseg * ((H + R - 1) / R);
+    const int64_t cost = (strips + ncu - 1) / ncu * (R + 3);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = R;
+    }
+  }
+  return best;
 }
 
 bool dwpw3_shape_ok(const ConvParams& P, int cin_pad) {
@@ -484,7 +497,7 @@ static bool d3_args_ok(const float* dww, const float* dwb) { return dww && dwb; 
 template <int N, int M, bool RS>
 static void launch_dwpw3(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
                          const float* dwb, hipStream_t st) {
-  const int R = d3_rows(P.H);
+  const int R = d3_rows(P.B, P.H, P.W);
   const int64_t want = (int64_t)((P.W + D3_TC - 1) / D3_TC) * ((P.H + R - 1) / R) * P.B;
   const int64_t g = std::min<int64_t>(want, (int64_t)d3_num_cus());
   const dim3 grid((unsigned)((g + 7) / 8 * 8));  // a multiple of 8: the XCD-aware deal
