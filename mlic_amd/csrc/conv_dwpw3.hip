@@ -44,6 +44,18 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 constexpr int D3_TC = 64;  // strip width: one pixel per producer lane = two MFMA column blocks
 constexpr int D3_G = 8;    // producer channels per A-image write (one 16-byte piece of hi and of lo)
 
+#ifndef MLIC_D3_FAKETAPS
+#define MLIC_D3_FAKETAPS 0
+#endif
+#ifndef MLIC_D3_ABL  // timing ablations (wrong results): 1 no producer row loads, 2 no consumer stores,
+#define MLIC_D3_ABL 0  // 4 no MFMAs, 8 no depthwise FMAs (the raw value written), 16 no A writes
+#endif
+#ifndef MLIC_D3_ASYNC  // 1: producer / consumer hand-off by LDS counters instead of one s_barrier per step
+#define MLIC_D3_ASYNC 0
+#endif
+#ifndef MLIC_D3_NBUF  // A images in the ring (2 or 3; the barrier form needs 2)
+#define MLIC_D3_NBUF (MLIC_D3_ASYNC ? 3 : 2)
+#endif
 #ifndef MLIC_D3_PK  // consumer epilogue on channel pairs with packed-fp32 VALU (A/B: 0 = scalar)
 #define MLIC_D3_PK 1
 #endif
@@ -67,6 +79,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t d3_rsrc(const float* base, uin
 }
 
 __device__ __forceinline__ void d3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS hand-off counters (MLIC_D3_ASYNC): every lane of a wave adds 1 (no exec-masked LDS operations in
+// the MFMA waves), so one wave's event counts 64.  The wait is bounded: a broken protocol reports
+// through the range flag instead of hanging the GPU.
+__device__ __forceinline__ void d3_signal(uint32_t* ctr) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's A writes / reads are done
+  __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool d3_wait_geq(const uint32_t* ctr, uint32_t target) {
+  uint32_t spins = 0;
+  for (;;) {
+    const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 22)) return false;
+  }
+  asm volatile("" ::: "memory");
+  return true;
+}
 
 // A image byte offset of pixel row n, channel half g (0: channels 0-7, 1: 8-15) in a 32 x 32-byte block;
 // the 16-byte halves swapped when (n >> 3) & 1 (conflict-free ds_read_b128 for the consumers)
@@ -107,11 +138,18 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
   constexpr int NC = N / 32;      // consumer waves (32 output channels each) = producer waves (32 inputs)
   constexpr int KS = N / 16;      // k-steps of 16 channels
   constexpr int AB = KS * 4096;   // one A image: [ks][block][hi / lo][1 KB]
-  constexpr int AIMG0 = 0, BIAS0 = 2 * AB;
+  constexpr int NBUF = MLIC_D3_NBUF;
+  constexpr int AIMG0 = 0, CTR0 = NBUF * AB, BIAS0 = CTR0 + 2 * NBUF * 4;
   constexpr int LDS = BIAS0 + N * 4;
   static_assert(LDS <= 160 * 1024, "dwpw3: LDS");
+  static_assert(MLIC_D3_ASYNC || NBUF == 2, "dwpw3: the barrier form alternates two A images");
   __shared__ __attribute__((aligned(16))) char sm[LDS];
   float* sbias = reinterpret_cast<float*>(sm + BIAS0);
+  // (ASYNC) filled[b]: 64 per producer that wrote A[b], freed[b]: 64 per consumer done reading it; the
+  // t-th output row of the workgroup (strip-major) goes through A[t % NBUF], its (t / NBUF)-th use
+  uint32_t* filled = reinterpret_cast<uint32_t*>(sm + CTR0);
+  uint32_t* freed = filled + NBUF;
+  if (threadIdx.x < 2 * NBUF) filled[threadIdx.x] = 0;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -182,7 +220,13 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     // never written (rows above the strip)
     // F: the sums two tap rows in (finished by this row), A: one tap row in.  After the row A holds the
     // sums two rows in and F the new ones: the caller swaps the roles (no register moves)
-    auto feed = [&](float (&F)[32], float (&A)[32], int buf, int ynext) {
+    bool pbad = false;
+    auto feed = [&](float (&F)[32], float (&A)[32], int t, int ynext) {
+      const int buf = t < 0 ? -1 : t % NBUF;
+#if MLIC_D3_ASYNC
+      // the image's previous use (row t - NBUF) read by every consumer
+      if (t >= NBUF) pbad |= !d3_wait_geq(freed + buf, 64u * NC * (uint32_t)(t / NBUF));
+#endif
       uint32_t so = row_off(ynext);
       uint32_t toff = (uint32_t)cb;
 #if MLIC_D3_TPF
@@ -217,8 +261,15 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
           const float* bg = tcur + 18;
 #else
           asm volatile("" : "+s"(toff));
+#if MLIC_D3_FAKETAPS  // timing probe only (wrong results): the taps as constants, no scalar loads
+          static constexpr float fk[20] = {.1f, .2f, .3f, .4f, .5f, .6f, .7f, .8f, .9f, .11f,
+                                           .12f, .13f, .14f, .15f, .16f, .17f, .18f, .19f, .21f, .22f};
+          const float* tg = fk;
+          const float* bg = fk + 18;
+#else
           const float* tg = dww + toff * 9;
           const float* bg = dwb + toff;
+#endif
 #endif
 #if MLIC_D3_PPK
           // the channel pair (j, j + 1) as packed-fp32 VALU: each v_pk_fma_f32 is the two channels' fma,
@@ -258,6 +309,9 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             d3_neighbours_k(j & 15, se[j >> 4], C, L, Rr);
             const float* tp = tg + f * 9;
             float a = F[j], bs = A[j], nw = 0.0f;
+#if MLIC_D3_ABL & 8
+            a = C; bs = L; nw = Rr;
+#else
             a = fmaf(tp[6], L, a);
             a = fmaf(tp[7], C, a);
             a = fmaf(tp[8], Rr, a);
@@ -267,6 +321,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             nw = fmaf(tp[0], L, nw);
             nw = fmaf(tp[1], C, nw);
             nw = fmaf(tp[2], Rr, nw);
+#endif
             o[f] = a + bg[f];
             // the channel's results pinned here (opaque, ordered): the arithmetic has no chain of its own
             // and would otherwise sink to its uses (the A write, the next row) past the fences, keeping
@@ -274,7 +329,9 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             asm volatile("" : "+v"(o[f]), "+v"(bs), "+v"(nw));
             A[j] = bs;
             F[j] = nw;
+#if !(MLIC_D3_ABL & 1)
             load_ch(j, so);
+#endif
           }
 #endif
           const float2v vv = {o[0], o[1]};
@@ -296,11 +353,19 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
         }
         if (buf >= 0) {  // (uniform)
           // k-step cb / 16 + g / 16, channel half (g / 8) & 1 (cb % 32 == 0)
-          char* a = sm + (buf ? AB : 0) + (g >> 4) * 4096 + ((g >> 3) & 1 ? aw1 : aw0);
-          *reinterpret_cast<half8*>(a) = hv8;
-          *reinterpret_cast<half8*>(a + 1024) = lv8;
+          char* a = sm + buf * AB + (g >> 4) * 4096 + ((g >> 3) & 1 ? aw1 : aw0);
+#if MLIC_D3_ABL & 16
+          if (hv8[0] == (_Float16)12345.0f)  // (practically never: keeps the depthwise live)
+#endif
+          {
+            *reinterpret_cast<half8*>(a) = hv8;
+            *reinterpret_cast<half8*>(a + 1024) = lv8;
+          }
         }
       }
+#if MLIC_D3_ASYNC
+      if (buf >= 0) d3_signal(filled + buf);
+#endif
     };
     d3_barrier();  // bias written by every wave
     for (int k = 0; k < nstrip; ++k) {
@@ -320,14 +385,17 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
       load_row(ys - 1);
       // the next row of step u: input row ys + u (none after the strip's last: a padding row)
       auto step = [&](int u, float (&F)[32], float (&A)[32]) {
-        if (u <= R + 1) feed(F, A, u >= 2 ? (u & 1) : -1, u + 1 <= R + 1 ? ys + u : -1);
+        if (u <= R + 1) feed(F, A, u >= 2 ? k * R + u - 2 : -1, u + 1 <= R + 1 ? ys + u : -1);
+#if !MLIC_D3_ASYNC
         if (u >= 2) d3_barrier();
+#endif
       };
       for (int u = 0; u < R + 3; u += 2) {  // two steps per trip: the sum roles alternate
         step(u, pa, pb);
         if (u + 1 < R + 3) step(u + 1, pb, pa);
       }
     }
+    range_report(P.rflag, pbad);
     return;
   }
 
@@ -363,9 +431,15 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     // the MFMAs (dwpw2's masked residual loads there gave wrong results in some rows)
     const auto rs_o = d3_rsrc(P.out + (int64_t)b * P.out_bs + (int64_t)(32 * cw) * HW, 32u * hw4);
     const auto rs_r = RES ? d3_rsrc(P.res + (int64_t)b * P.res_bs + (int64_t)(32 * cw) * HW, 32u * hw4) : rs_o;
+#if !MLIC_D3_ASYNC
     d3_barrier();  // the strip's A[0]
+#endif
     for (int s = 0; s < R; ++s) {
       const int y = ys + s;
+      const int t = k * R + s, buf = t % NBUF;
+#if MLIC_D3_ASYNC
+      bad |= !d3_wait_geq(filled + buf, 64u * NC * (uint32_t)(t / NBUF + 1));
+#endif
 #pragma unroll
       for (int bk = 0; bk < 2; ++bk) {
         __builtin_amdgcn_sched_barrier(0);  // the two blocks one after the other (one accumulator live)
@@ -384,7 +458,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             so += (q & 3) == 3 ? 5u * hw4 : hw4;
           }
         }
-        const char* a = sm + AIMG0 + (s & 1) * AB + bk * 2048 + aoff;
+        const char* a = sm + AIMG0 + buf * AB + bk * 2048 + aoff;
         floatx16 acc;
         // the B fragments one k-step ahead of their MFMAs
         half8 ah = *reinterpret_cast<const half8*>(a);
@@ -397,9 +471,14 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             nl = *reinterpret_cast<const half8*>(a + (ks + 1) * 4096 + 1024);
           }
           // pw_resident's term order: (W lo . X hi), (W hi . X lo), (W hi . X hi)
+#if MLIC_D3_ABL & 4
+          if (ks == 0) acc = floatx16{};
+          acc[ks & 15] += (float)ah[0] + (float)al[1] + (float)bwh[ks][0] + (float)bwl[ks][1];
+#else
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bwl[ks], ah, ks == 0 ? floatx16{} : acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bwh[ks], al, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bwh[ks], ah, acc, 0, 0, 0);
+#endif
           ah = nh;
           al = nl;
         }
@@ -428,6 +507,9 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
               // element 0 whatever f is -- seen in the ISA)
               const float tv = t2[f];
               bad |= ok && !(__builtin_fabsf(tv) <= 3.4e38f);
+#if MLIC_D3_ABL & 2
+              if (tv == 12345.0f)
+#endif
               __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tv), rs_o, vo, so, 0);
               so += hw4;
             }
@@ -448,7 +530,11 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
           so += 4u * hw4;
         }
       }
+#if MLIC_D3_ASYNC
+      d3_signal(freed + buf);
+#else
       d3_barrier();
+#endif
     }
   }
   range_report(P.rflag, bad);
