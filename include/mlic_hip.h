@@ -103,7 +103,10 @@ int mlic_set_poison(mlic_model* m, int on);
  * reprojection conv's packed operand ($MLIC_LINATT_FUSED); "dw_strip" = the register-strip depthwise
  * 3x3 for stride-1 planes up to 64 columns ($MLIC_DW_STRIP); "x4_splitk" = split-K for few-tile
  * 3x3 / 5x5 convs (default off, $MLIC_X4_SPLITK=1) -- set it before a handle's first call (the
- * workspace is sized for the setting in force then) */
+ * workspace is sized for the setting in force then); "dwpw2" = the form of the fused depthwise +
+ * pointwise for Cin = Cout in {96, 128, 160, 192} (-1 default = $MLIC_DWPW2 or 2: the register-row
+ * dwpw3_kernel; 1 the row-pipelined LDS form; 0 the round-4 dwpw_kernel) -- every form gives the same
+ * bits */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
  * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the
