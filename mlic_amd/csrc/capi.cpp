@@ -232,6 +232,7 @@ int mlic_set_kernel_option(const char* name, int value) {
     else if (n == "dw_strip") dw_set_strip(value);
     else if (n == "x4_splitk") x4_set_splitk(value);
     else if (n == "dwpw2") dwpw2_set(value);
+    else if (n == "pw3") pw3_set(value);
     else throw Error("mlic: unknown kernel option " + n);
   });
 }

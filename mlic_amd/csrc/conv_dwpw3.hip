@@ -129,8 +129,10 @@ __device__ __forceinline__ void d3_neighbours_k(int k, float e, float v, float& 
 }
 }  // namespace
 
-// MODE: 0 = bias only, 1 = GELU (dwpw_kernel's modes); RES: residual add last
-template <int N, int MODE, bool RES>
+// MODE: 0 = bias only, 1 = GELU (dwpw_kernel's modes), 2 = GDN, 3 = IGDN (pw_resident's: x * rsqrt(v),
+// x * sqrt(v), the aux operand x = the conv input); RES: residual add last.  PW: the pointwise conv
+// alone (no depthwise; MODE 2 / 3 convolve x * x) -- the full-resolution GDN / IGDN of g_a / g_s
+template <int N, int MODE, bool RES, bool PW = false>
 __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R, const _Float16* __restrict__ wh,
                                                            const _Float16* __restrict__ wl, int cin_pad,
                                                            const float* __restrict__ dww,
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     auto load_ch = [&](int j, uint32_t& so) {
       asm volatile("" : "+s"(so));
       sc[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, cxo, so, 0));
-      if ((j & 15) == 15)
+      if (!PW && (j & 15) == 15)
         se[j >> 4] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, exo, so - 15u * hw4, 0));
       so += hw4;
     };
@@ -367,7 +369,56 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
       if (buf >= 0) d3_signal(filled + buf);
 #endif
     };
+    // PW: the input row held in sc (x, or x * x for GDN / IGDN), split into A `buf`; then input row `ynext`
+    auto feed_pw = [&](int t, int ynext) {
+      const int buf = t % NBUF;
+      uint32_t so = row_off(ynext);
+#pragma unroll
+      for (int g = 0; g < 32; g += D3_G) {
+        __builtin_amdgcn_sched_barrier(0);
+        half8 hv8, lv8;
+#pragma unroll
+        for (int e = 0; e < D3_G; e += 2) {
+          float o[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            const int j = g + e + f;
+            float v = sc[j];
+            if constexpr (MODE == 2 || MODE == 3) v *= v;
+            o[f] = v;
+            load_ch(j, so);
+          }
+          const float2v vv = {o[0], o[1]};
+          const half2v hv = __builtin_convertvector(vv, half2v);
+          const half2v lv = __builtin_convertvector(vv - __builtin_convertvector(hv, float2v), half2v);
+          hv8[e] = hv[0];
+          hv8[e + 1] = hv[1];
+          lv8[e] = lv[0];
+          lv8[e + 1] = lv[1];
+        }
+        char* a = sm + buf * AB + (g >> 4) * 4096 + ((g >> 3) & 1 ? aw1 : aw0);
+        *reinterpret_cast<half8*>(a) = hv8;
+        *reinterpret_cast<half8*>(a + 1024) = lv8;
+      }
+    };
     d3_barrier();  // bias written by every wave
+    if constexpr (PW) {
+      // rows ys .. ys + R - 1, one per step; R + 1 barriers per strip as the consumers' (the strip's A
+      // after row 0, then one per consumed row)
+      for (int k = 0; k < nstrip; ++k) {
+        int b, ys, x0;
+        strip_of(k, b, ys, x0);
+        rs = d3_rsrc(P.seg[0].p + (int64_t)b * P.seg[0].bs + (int64_t)cb * HW, 32u * hw4);
+        const int xl = x0 + lane;
+        cxo = xl < W ? (uint32_t)xl * 4u : 0x80000000u;
+        load_row(ys);
+        for (int u = 0; u <= R; ++u) {
+          if (u < R) feed_pw(k * R + u, u + 1 < R ? ys + u + 1 : -1);
+          d3_barrier();
+        }
+      }
+      return;
+    }
     for (int k = 0; k < nstrip; ++k) {
       int b, ys, x0;
       strip_of(k, b, ys, x0);
@@ -431,6 +482,8 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
     // the MFMAs (dwpw2's masked residual loads there gave wrong results in some rows)
     const auto rs_o = d3_rsrc(P.out + (int64_t)b * P.out_bs + (int64_t)(32 * cw) * HW, 32u * hw4);
     const auto rs_r = RES ? d3_rsrc(P.res + (int64_t)b * P.res_bs + (int64_t)(32 * cw) * HW, 32u * hw4) : rs_o;
+    constexpr bool GDN = MODE == 2 || MODE == 3;
+    const auto rs_x = GDN ? d3_rsrc(P.aux + (int64_t)b * P.aux_bs + (int64_t)(32 * cw) * HW, 32u * hw4) : rs_o;
 #if !MLIC_D3_ASYNC
     d3_barrier();  // the strip's A[0]
 #endif
@@ -448,7 +501,16 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
         const int px = x0 + 32 * bk + n;
         const bool ok = y < H && px < W;
         const uint32_t vo = ok ? (uint32_t)(y * W + px) * 4u + (uint32_t)(4 * h) * hw4 : 0x80000000u;
-        float xr[16];
+        float xr[16], xa[16];
+        if constexpr (GDN) {  // the GDN / IGDN input x of the block's output channels
+          uint32_t so = 0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            asm volatile("" : "+s"(so));
+            xa[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_x, vo, so, 0));
+            so += (q & 3) == 3 ? 5u * hw4 : hw4;
+          }
+        }
         if constexpr (RES) {
           uint32_t so = 0;
 #pragma unroll
@@ -490,6 +552,20 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
         for (int g = 0; g < 4; ++g) {
           const float4 b4 = *reinterpret_cast<const float4*>(sb + 8 * g);
           const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+          if constexpr (GDN) {
+            // pw_resident's GDN epilogue: the range check on the pre-activation, x * rsqrt(v) / x * sqrt(v)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int q = 4 * g + e;
+              asm volatile("" : "+s"(so));
+              float tv = __builtin_fmaf(acc[q], unscale, bq[e]);
+              bad |= ok && !(__builtin_fabsf(tv) <= 3.4e38f);
+              tv = gdn_apply(xa[q], tv, MODE == 3);
+              if constexpr (RES) tv = tv + xr[q];
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tv), rs_o, vo, so, 0);
+              so += hw4;
+            }
+          } else {
 #if MLIC_D3_PK
           // channel pairs: the scale / bias FMA, GELU and residual add as packed-fp32 VALU (gelu_erf2: the
           // same operations element for element)
@@ -527,6 +603,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
             so += hw4;
           }
 #endif
+          }
           so += 4u * hw4;
         }
       }
@@ -604,6 +681,56 @@ void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, 
   }
   D3_RUN(192) D3_RUN(160) D3_RUN(128) D3_RUN(96)
 #undef D3_RUN
+}
+
+// the pointwise form (PW) for the full-resolution GDN / IGDN (pw_resident's MODE 2 / 3, with or without
+// residual): $MLIC_PW3 / mlic_set_kernel_option("pw3") (-1 default = env or on; 0 = pw_resident)
+static int g_pw3 = -1;
+void pw3_set(int on) { g_pw3 = on; }
+static bool pw3_enabled() {
+  static const bool env = [] {
+    const char* e = std::getenv("MLIC_PW3");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return g_pw3 < 0 ? env : g_pw3 != 0;
+}
+static int pw3_mode(const ConvParams& P) {
+  const int e = P.epi & ~EPI_RES;
+  if (e == (EPI_GDN | EPI_SQUARE_IN)) return 2;
+  if (e == (EPI_IGDN | EPI_SQUARE_IN)) return 3;
+  return -1;
+}
+bool pw3_ok(const ConvParams& P, int cin_pad) {
+  if (!pw3_enabled() || pw3_mode(P) < 0 || !P.aux) return false;
+  if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
+  if (P.Cin != P.Cout || (P.Cin != 96 && P.Cin != 128 && P.Cin != 160 && P.Cin != 192)) return false;
+  if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W) return false;
+  if ((int64_t)P.H * P.W < 16384) return false;  // the full-resolution grids (as the fused dwsep rule)
+  if ((int64_t)P.Cin * P.H * P.W * 4 >= (1ll << 31)) return false;
+  return true;
+}
+template <int N, int M, bool RS>
+static void launch_pw3(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
+  const int R = d3_rows(P.B, P.H, P.W);
+  const int64_t want = (int64_t)((P.W + D3_TC - 1) / D3_TC) * ((P.H + R - 1) / R) * P.B;
+  const int64_t g = std::min<int64_t>(want, (int64_t)d3_num_cus());
+  const dim3 grid((unsigned)((g + 7) / 8 * 8));
+  hipLaunchKernelGGL((dwpw3_kernel<N, M, RS, true>), grid, dim3(N / 16 * 64), 0, st, P, R, wh, wl, cin_pad,
+                     (const float*)nullptr, (const float*)nullptr);
+  HIP_OK(hipGetLastError());
+}
+void pw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
+  MLIC_CHECK(pw3_ok(P, cin_pad), "pw3: unsupported shape");
+  const int mode = pw3_mode(P), res = (P.epi & EPI_RES) ? 1 : 0;
+#define P3_RUN(NN)                                                                \
+  if (P.Cin == NN) {                                                              \
+    if (mode == 2 && !res) return launch_pw3<NN, 2, false>(P, wh, wl, cin_pad, st); \
+    if (mode == 2 && res) return launch_pw3<NN, 2, true>(P, wh, wl, cin_pad, st);   \
+    if (mode == 3 && !res) return launch_pw3<NN, 3, false>(P, wh, wl, cin_pad, st); \
+    return launch_pw3<NN, 3, true>(P, wh, wl, cin_pad, st);                          \
+  }
+  P3_RUN(192) P3_RUN(160) P3_RUN(128) P3_RUN(96)
+#undef P3_RUN
 }
 
 }  // namespace mlic

@@ -375,6 +375,7 @@ static void launch_pw(const ConvParams& P, const _Float16* wh, const _Float16* w
 
 void pw_resident_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st) {
   MLIC_CHECK(pw_resident_ok(P, cin_pad), "pw_resident: unsupported shape");
+  if (pw3_ok(P, cin_pad)) return pw3_forward(P, wh, wl, cin_pad, st);  // full-resolution GDN / IGDN
   const int mode = pw_mode(P);
   const int ct = (P.Cout + 31) / 32;
   const int res = (P.epi & EPI_RES) ? 1 : 0;

@@ -434,6 +434,25 @@ def test_dwpw2_fused(B, Cn, H, W, epi, form):
         _lib.call("mlic_set_kernel_option", b"dwpw2", -1)
 
 
+@pytest.mark.parametrize("B,Cn,H,W,epi", [
+    (1, 192, 136, 128, GDN | SQUARE | RES), (2, 192, 130, 130, IGDN | SQUARE | RES), (1, 160, 128, 200, GDN | SQUARE),
+    (1, 128, 200, 100, IGDN | SQUARE), (2, 96, 64, 300, GDN | SQUARE | RES)])
+def test_pw3_gdn(B, Cn, H, W, epi):
+    """The full-resolution GDN / IGDN 1x1 on the register-row kernel's pointwise form (conv_dwpw3.hip, PW):
+    bit for bit pw_resident's (x^2 split, MFMA order, x * rsqrt / sqrt epilogue, residual last), and
+    within tolerance of the float64 reference."""
+    from mlic_amd import _lib
+    try:
+        _lib.call("mlic_set_kernel_option", b"pw3", 0)
+        y0, ref = run(PW, B, Cn, Cn, H, W, 1, epi=epi, seed=3)
+        _lib.call("mlic_set_kernel_option", b"pw3", 1)
+        y1, _ = run(PW, B, Cn, Cn, H, W, 1, epi=epi, seed=3)
+    finally:
+        _lib.call("mlic_set_kernel_option", b"pw3", -1)
+    check(y1, ref)
+    assert torch.equal(y0, y1)
+
+
 # the latent-resolution dwsep convs with Cin != Cout: the LRP's 224 -> 128 GELU and its 128 -> 32 head
 # (0.5 tanh, checkerboard mask, residual; quantization.py:30-45), the channel context's 192 -> 128 GELU
 @pytest.mark.parametrize("B,Cin,Cout,H,W,epi", [
