@@ -683,8 +683,8 @@ void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, 
 #undef D3_RUN
 }
 
-// the pointwise form (PW) for the full-resolution GDN / IGDN (pw_resident's MODE 2 / 3, with or without
-// residual): $MLIC_PW3 / mlic_set_kernel_option("pw3") (-1 default = env or on; 0 = pw_resident)
+// the pointwise form (PW) for the full-resolution 1x1 convs with Cin = Cout (pw_resident's MODE 0 - 3: bias,
+// GELU, GDN, IGDN, with or without residual): $MLIC_PW3 / mlic_set_kernel_option("pw3") (-1 default = env or on; 0 = pw_resident)
 static int g_pw3 = -1;
 void pw3_set(int on) { g_pw3 = on; }
 static bool pw3_enabled() {
@@ -696,12 +696,15 @@ static bool pw3_enabled() {
 }
 static int pw3_mode(const ConvParams& P) {
   const int e = P.epi & ~EPI_RES;
+  if (e == EPI_NONE) return 0;
+  if (e == EPI_GELU) return 1;
   if (e == (EPI_GDN | EPI_SQUARE_IN)) return 2;
   if (e == (EPI_IGDN | EPI_SQUARE_IN)) return 3;
   return -1;
 }
 bool pw3_ok(const ConvParams& P, int cin_pad) {
-  if (!pw3_enabled() || pw3_mode(P) < 0 || !P.aux) return false;
+  const int mode = pw3_mode(P);
+  if (!pw3_enabled() || mode < 0 || (mode >= 2 && !P.aux)) return false;
   if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.Cin != P.Cout || (P.Cin != 96 && P.Cin != 128 && P.Cin != 160 && P.Cin != 192)) return false;
   if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W) return false;
@@ -724,6 +727,10 @@ void pw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, in
   const int mode = pw3_mode(P), res = (P.epi & EPI_RES) ? 1 : 0;
 #define P3_RUN(NN)                                                                \
   if (P.Cin == NN) {                                                              \
+    if (mode == 0 && !res) return launch_pw3<NN, 0, false>(P, wh, wl, cin_pad, st); \
+    if (mode == 0 && res) return launch_pw3<NN, 0, true>(P, wh, wl, cin_pad, st);   \
+    if (mode == 1 && !res) return launch_pw3<NN, 1, false>(P, wh, wl, cin_pad, st); \
+    if (mode == 1 && res) return launch_pw3<NN, 1, true>(P, wh, wl, cin_pad, st);   \
     if (mode == 2 && !res) return launch_pw3<NN, 2, false>(P, wh, wl, cin_pad, st); \
     if (mode == 2 && res) return launch_pw3<NN, 2, true>(P, wh, wl, cin_pad, st);   \
     if (mode == 3 && !res) return launch_pw3<NN, 3, false>(P, wh, wl, cin_pad, st); \

@@ -436,7 +436,8 @@ def test_dwpw2_fused(B, Cn, H, W, epi, form):
 
 @pytest.mark.parametrize("B,Cn,H,W,epi", [
     (1, 192, 136, 128, GDN | SQUARE | RES), (2, 192, 130, 130, IGDN | SQUARE | RES), (1, 160, 128, 200, GDN | SQUARE),
-    (1, 128, 200, 100, IGDN | SQUARE), (2, 96, 64, 300, GDN | SQUARE | RES)])
+    (1, 128, 200, 100, IGDN | SQUARE), (2, 96, 64, 300, GDN | SQUARE | RES),
+    (2, 192, 136, 240, GELU), (1, 192, 130, 140, 0), (1, 160, 128, 130, GELU | RES)])
 def test_pw3_gdn(B, Cn, H, W, epi):
     """The full-resolution GDN / IGDN 1x1 on the register-row kernel's pointwise form (conv_dwpw3.hip, PW):
     bit for bit pw_resident's (x^2 split, MFMA order, x * rsqrt / sqrt epilogue, residual last), and
