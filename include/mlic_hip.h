@@ -106,8 +106,9 @@ int mlic_set_poison(mlic_model* m, int on);
  * workspace is sized for the setting in force then); "dwpw2" = the form of the fused depthwise +
  * pointwise for Cin = Cout in {96, 128, 160, 192} (-1 default = $MLIC_DWPW2 or 2: the register-row
  * dwpw3_kernel; 1 the row-pipelined LDS form; 0 the round-4 dwpw_kernel) -- every form gives the same
- * bits; "pw3" = the full-resolution GDN / IGDN 1x1 on that kernel's pointwise form (-1 default =
- * $MLIC_PW3 or on; 0 = pw_resident, the same bits) */
+ * bits; "pw3" = the full-resolution 1x1 convs with Cin = Cout (GDN / IGDN at 544 x 960) on that kernel's
+ * pointwise form (-1 default = $MLIC_PW3 or 1: from 256 K px per image; 2: every grid; 0 = pw_resident,
+ * the same bits) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
  * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the

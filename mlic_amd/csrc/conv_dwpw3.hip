@@ -685,14 +685,16 @@ void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, 
 
 // the pointwise form (PW) for the full-resolution 1x1 convs with Cin = Cout (pw_resident's MODE 0 - 3: bias,
 // GELU, GDN, IGDN, with or without residual): $MLIC_PW3 / mlic_set_kernel_option("pw3") (-1 default = env or on; 0 = pw_resident)
+// residual)'s setting: 0 off, 1 on from 256 K px per image (at 272 x 480 pw_resident measured faster: 0.45 vs
+// 0.48 ms GELU, 0.64 vs 0.66 GDN; at 544 x 960 pw3 GDN / IGDN 2.07 vs 2.30), 2 on at every grid (tests)
 static int g_pw3 = -1;
 void pw3_set(int on) { g_pw3 = on; }
-static bool pw3_enabled() {
-  static const bool env = [] {
+static int pw3_setting() {
+  static const int env = [] {
     const char* e = std::getenv("MLIC_PW3");
-    return !(e && std::atoi(e) == 0);
+    return e ? std::atoi(e) : 1;
   }();
-  return g_pw3 < 0 ? env : g_pw3 != 0;
+  return g_pw3 < 0 ? env : g_pw3;
 }
 static int pw3_mode(const ConvParams& P) {
   const int e = P.epi & ~EPI_RES;
@@ -703,12 +705,12 @@ static int pw3_mode(const ConvParams& P) {
   return -1;
 }
 bool pw3_ok(const ConvParams& P, int cin_pad) {
-  const int mode = pw3_mode(P);
-  if (!pw3_enabled() || mode < 0 || (mode >= 2 && !P.aux)) return false;
+  const int mode = pw3_mode(P), setting = pw3_setting();
+  if (setting == 0 || mode < 0 || (mode >= 2 && !P.aux)) return false;
+  if (setting == 1 && (int64_t)P.H * P.W < 262144) return false;
   if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.Cin != P.Cout || (P.Cin != 96 && P.Cin != 128 && P.Cin != 160 && P.Cin != 192)) return false;
   if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W) return false;
-  if ((int64_t)P.H * P.W < 16384) return false;  // the full-resolution grids (as the fused dwsep rule)
   if ((int64_t)P.Cin * P.H * P.W * 4 >= (1ll << 31)) return false;
   return true;
 }

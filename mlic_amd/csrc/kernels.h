@@ -51,9 +51,9 @@ bool dwpw2_ok(const ConvParams& P, int cin_pad);
 // LDS form (conv_dwpw2.hip), 2 = the register-row form (conv_dwpw3.hip)
 void dwpw2_set(int on);
 bool dwpw3_shape_ok(const ConvParams& P, int cin_pad);
-// the same kernel's pointwise-only form for the full-resolution GDN / IGDN 1x1 (pw_resident MODE 2 / 3,
-// Cin = Cout in {96, 128, 160, 192}, >= 16 K px): pw_resident_forward takes it where pw3_ok;
-// mlic_set_kernel_option("pw3"): -1 = $MLIC_PW3 (default on), 0 off, 1 on
+// the same kernel's pointwise-only form for the full-resolution 1x1 convs (pw_resident MODE 0 - 3, Cin = Cout
+// in {96, 128, 160, 192}): pw_resident_forward takes it where pw3_ok; mlic_set_kernel_option("pw3"):
+// -1 = $MLIC_PW3 (default 1), 0 off, 1 from 256 K px per image, 2 every grid
 bool pw3_ok(const ConvParams& P, int cin_pad);
 void pw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, hipStream_t st);
 void pw3_set(int on);

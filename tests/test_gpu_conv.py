@@ -446,7 +446,7 @@ def test_pw3_gdn(B, Cn, H, W, epi):
     try:
         _lib.call("mlic_set_kernel_option", b"pw3", 0)
         y0, ref = run(PW, B, Cn, Cn, H, W, 1, epi=epi, seed=3)
-        _lib.call("mlic_set_kernel_option", b"pw3", 1)
+        _lib.call("mlic_set_kernel_option", b"pw3", 2)  # (2: at every grid; the default takes >= 256 K px)
         y1, _ = run(PW, B, Cn, Cn, H, W, 1, epi=epi, seed=3)
     finally:
         _lib.call("mlic_set_kernel_option", b"pw3", -1)

@@ -25,7 +25,7 @@ def timeit(fn, iters=10):
 
 
 def main():
-    B, Cn, H, W = 8, 192, 544, 960
+    B, Cn, H, W = [int(v) for v in os.environ.get("PW3_SHAPE", "8,192,544,960").split(",")]
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(0)
     x = ((torch.rand(B, Cn, H, W, generator=g) - 0.5) * 4).to(dev)
@@ -38,7 +38,7 @@ def main():
     for rnd in range(2):
         for on in (0, 1):
             _lib.call("mlic_set_kernel_option", b"pw3", on)
-            for epi in (GDN | SQUARE | RES, IGDN | SQUARE | RES):
+            for epi in [int(e, 0) for e in os.environ.get("PW3_EPI", "0x142,0x144").split(",")]:
                 f = lambda: _lib.call("mlic_conv_run", P(st), 3, P(x.data_ptr()), P(w.data_ptr()), P(b.data_ptr()),  # noqa
                                       P(y.data_ptr()), B, Cn, Cn, H, W, 1, 1, epi, P(x.data_ptr()), P(r.data_ptr()))
                 t = timeit(f)
