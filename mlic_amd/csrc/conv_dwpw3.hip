@@ -684,9 +684,9 @@ void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, 
 }
 
 // the pointwise form (PW) for the full-resolution 1x1 convs with Cin = Cout (pw_resident's MODE 0 - 3: bias,
-// GELU, GDN, IGDN, with or without residual): $MLIC_PW3 / mlic_set_kernel_option("pw3") (-1 default = env or on; 0 = pw_resident)
-// residual)'s setting: 0 off, 1 on from 256 K px per image (at 272 x 480 pw_resident measured faster: 0.45 vs
-// 0.48 ms GELU, 0.64 vs 0.66 GDN; at 544 x 960 pw3 GDN / IGDN 2.07 vs 2.30), 2 on at every grid (tests)
+// GELU, GDN, IGDN, with or without residual).  $MLIC_PW3 / mlic_set_kernel_option("pw3"): 0 off, 1 (default)
+// from 256 K px per image (at 272 x 480 pw_resident measured faster: 0.45 vs 0.48 ms GELU, 0.64 vs 0.66 GDN;
+// at 544 x 960 pw3's GDN / IGDN 2.07 vs 2.30), 2 at every grid (tests)
 static int g_pw3 = -1;
 void pw3_set(int on) { g_pw3 = on; }
 static int pw3_setting() {
