@@ -226,6 +226,14 @@ void eb_forward(const EbParams& P, hipStream_t st);
 void eb_dequant(const int32_t* sym, const float* quantiles, float* z_hat, int C, int HW, int B, hipStream_t st);
 
 void pack_conv(const float* w, float* out, int Cout, int Cin, int KK, hipStream_t st);
+// many device-to-device float copies in one launch (the weight load's per-parameter copies: one kernel
+// instead of a blit per tensor); `descs` is a device array of n {dst, src, count}
+struct CopyDesc {
+  float* dst;
+  const float* src;
+  int64_t n;
+};
+void copy_many(const CopyDesc* descs, int n, hipStream_t st);
 void gdn_prep(const float* beta, const float* gamma, const float* bb, const float* bped, const float* gb,
               const float* gped, float* beta_eff, float* gamma_pk, float* gamma_eff, int C, hipStream_t st);
 void local_mask(float* out, int H, int W, hipStream_t st);

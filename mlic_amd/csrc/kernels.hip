@@ -881,6 +881,18 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict_
   out[((int64_t)tap * Cin + ci) * Cout + co] = w[i];
 }
 
+__global__ void copy_many_kernel(const CopyDesc* __restrict__ d) {
+  const CopyDesc c = d[blockIdx.x];
+  for (int64_t i = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; i < c.n; i += (int64_t)gridDim.y * blockDim.x)
+    c.dst[i] = c.src[i];
+}
+
+void copy_many(const CopyDesc* descs, int n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)n, 16), dim3(256), 0, st, descs);
+  HIP_OK(hipGetLastError());
+}
+
 void pack_conv(const float* w, float* out, int Cout, int Cin, int KK, hipStream_t st) {
   const int64_t n = (int64_t)Cout * Cin * KK;
   hipLaunchKernelGGL(pack_conv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, out, Cout, Cin, KK);

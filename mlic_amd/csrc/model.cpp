@@ -98,6 +98,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
   auto shape = [&](int i, int d) { return (int)shapes[i * 4 + d]; };
 
   std::map<std::string, std::pair<const float*, int>> ep0;  // EntropyParameters layer-0 weights (hoisting)
+  std::vector<CopyDesc> copies;  // plain parameter copies, made by one launch after the loop
   for (int i = 0; i < n; ++i) {
     const std::string k = names[i];
     float* dst = take(numel[i]);
@@ -106,7 +107,7 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
     const std::string base = k.substr(0, k.rfind('.'));
     if (ends_with(k, ".weight") && ndims[i] == 4 && shape(i, 1) == 1 && shape(i, 0) > 1) {
       // depthwise [C,1,3,3]
-      HIP_OK(hipMemcpyAsync(dst, ptrs[i], numel[i] * 4, hipMemcpyDeviceToDevice, st));
+      copies.push_back(CopyDesc{dst, ptrs[i], numel[i]});
       DwW w;
       w.w = dst;
       w.C = shape(i, 0);
@@ -144,9 +145,18 @@ Model::Model(const std::string& name, int n, const char* const* names, const flo
       w.name = base;
       convs_[base] = w;
     } else {
-      HIP_OK(hipMemcpyAsync(dst, ptrs[i], numel[i] * 4, hipMemcpyDeviceToDevice, st));
+      copies.push_back(CopyDesc{dst, ptrs[i], numel[i]});
       raw_[k] = dst;
     }
+  }
+  if (!copies.empty()) {
+    // (before any kernel below reads a copied parameter: same stream)
+    CopyDesc* dd = nullptr;
+    HIP_OK(hipMalloc(&dd, copies.size() * sizeof(CopyDesc)));
+    owned_.push_back(dd);
+    HIP_OK(hipMemcpyAsync(dd, copies.data(), copies.size() * sizeof(CopyDesc), hipMemcpyHostToDevice, st));
+    copy_many(dd, (int)copies.size(), st);
+    HIP_OK(hipStreamSynchronize(st));  // the host vector of descriptors dies here
   }
   // biases
   for (auto& kv : convs_) {
