@@ -883,13 +883,20 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict_
 
 __global__ void copy_many_kernel(const CopyDesc* __restrict__ d) {
   const CopyDesc c = d[blockIdx.x];
-  for (int64_t i = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; i < c.n; i += (int64_t)gridDim.y * blockDim.x)
-    c.dst[i] = c.src[i];
+  const int64_t t0 = (int64_t)blockIdx.y * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.y * blockDim.x;
+  if (((reinterpret_cast<uintptr_t>(c.dst) | reinterpret_cast<uintptr_t>(c.src)) & 15) == 0) {
+    const int64_t n4 = c.n >> 2;  // 16-byte pieces, then the tail
+    for (int64_t i = t0; i < n4; i += nt)
+      reinterpret_cast<float4*>(c.dst)[i] = reinterpret_cast<const float4*>(c.src)[i];
+    for (int64_t i = 4 * n4 + t0; i < c.n; i += nt) c.dst[i] = c.src[i];
+  } else {
+    for (int64_t i = t0; i < c.n; i += nt) c.dst[i] = c.src[i];
+  }
 }
 
 void copy_many(const CopyDesc* descs, int n, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)n, 16), dim3(256), 0, st, descs);
+  hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)n, 128), dim3(256), 0, st, descs);
   HIP_OK(hipGetLastError());
 }
 
