@@ -62,10 +62,12 @@ def family(cat_name: str) -> str:
 
 
 WORKLOADS = {
-    # the 32 images of a step as 4 request streams of 8 (2 lanes each): a stream's decompress starts as
-    # soon as its own compress + rANS encode is done, instead of every lane waiting for the slowest
-    # lane's encode (measured 86.9-88.1 img/s against 83.0-85.7 as one 32-image call on 4 lanes)
-    "main": dict(model="MLICPP_L", groups=[(1088, 1920, 32)], scaling="weak", split=4, lanes=2,
+    # the 32 images of a step as 4 request streams of 8: a stream's decompress starts as soon as its own
+    # compress + rANS encode is done, instead of every lane waiting for the slowest lane's encode
+    # (measured 86.9-88.1 img/s against 83.0-85.7 as one 32-image call on 4 lanes).  One lane per stream
+    # since round 5 (faster kernels: 101.5-101.7 against 99.7-100.4 with 2 lanes, 94.2 with 3; 8 streams
+    # of 4: 96.2-96.3; alternating on one box, profiles/r05/ab/host_schedule_ab.log)
+    "main": dict(model="MLICPP_L", groups=[(1088, 1920, 32)], scaling="weak", split=4, lanes=1,
                  desc="config 2: MLICPP_L compress+decompress of 1920x1088 images"),
     "kodak": dict(model="MLICPP_L", groups=[(512, 768, 64)], scaling="weak",
                   desc="config 1 shape on GPU: MLICPP_L compress+decompress of 768x512 (Kodak-size) images"),
@@ -81,8 +83,9 @@ WORKLOADS = {
     # (322.6 / 322.8 against 299.9 with 1)
     "kodak-sweep": dict(model="MLICPP_L", scaling="strong", lanes=2, lanes_many=1, group_concurrency=6,
                         desc="config 4: MLICPP_L 24 Kodak-size images x 6 lambda stand-ins, LPT-sharded"),
-    # (4 request streams of 1-3 images, 2 lanes each: 40.2-40.4 img/s against 39.4-39.6 as two batches)
-    "vbr-mixed": dict(model="MLICPP_L_VBR", groups=[(2176, 3840, 2), (1088, 1920, 6)], scaling="weak", split=2, lanes=2,
+    # (4 request streams of 1-3 images: 40.2-40.4 img/s against 39.4-39.6 as two batches; one lane per
+    # stream since round 5: 43.3-44.1 against 41.9-42.3 with 2)
+    "vbr-mixed": dict(model="MLICPP_L_VBR", groups=[(2176, 3840, 2), (1088, 1920, 6)], scaling="weak", split=2, lanes=1,
                       desc="config 5: MLICPP_L_VBR 4K + 1080p batch, one VBR level per image"),
 }
 
