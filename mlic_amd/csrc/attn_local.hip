@@ -226,12 +226,15 @@ constexpr int LP_TW = 32, LP_LW = LP_TW + 4, LP_NCELL = 5 * LP_LW, LP_NCP = LP_N
 // gathered 2 bytes at a time straight into the fragment.  Interior pixels take the checkerboard /
 // window mask from per-lane bit masks (parity only); the two rows / columns at the border compute
 // the in-image tests.
-__global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttnParams P, _Float16* __restrict__ outp,
+__global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void local_attn_packed_kernel(LocalAttnParams P, _Float16* __restrict__ outp,
                                                                      int npos) {
   constexpr int QKP = LP_NCP * 16;       // halves per (tensor, head, hi|lo) plane
   constexpr int QK_H = 2 * 2 * 2 * QKP;  // q, k x heads x hi|lo
   constexpr int VP = 32 * LP_NCP;        // halves per v plane (hi or lo)
   __shared__ __attribute__((aligned(16))) _Float16 sm[QK_H + 2 * VP];
+  // relative-position bias of (query l32, key j of register r), per lane: [head][r][lane] (8 KB;
+  // held in registers it pushed the kernel past 128 VGPRs, i.e. one workgroup per CU)
+  __shared__ float sbias[2 * 16 * 64];
   const int H = P.H, W = P.W, HW = H * W;
   const int b = blockIdx.y;
   const int ntx = (W + LP_TW - 1) / LP_TW;
@@ -250,6 +253,11 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
       const int gy = y0 - 2 + cell / LP_LW, gx = x0 - 2 + cell % LP_LW;
       if (gy >= 0 && gy < H && gx >= 0 && gx < W) stg[q] = src[(int64_t)ch * HW + gy * W + gx];
     }
+  }
+  for (int i = threadIdx.x; i < 2 * 16 * 64; i += LA_THREADS) {
+    const int hh = i >> 10, r = (i >> 6) & 15, ln = i & 63, q32 = ln & 31;
+    const int j = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+    sbias[i] = (q32 < 25 && j < 25) ? P.rel_table[P.rel_index[q32 * 25 + j] * 2 + hh] : 0.0f;
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -275,23 +283,13 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
   const int l32 = lane & 31, h = lane >> 5;
   const bool lvalid = l32 < 25;
   const int cy = lvalid ? l32 / 5 : 0, cx = lvalid ? l32 % 5 : 0;
-  // relative-position bias (query i = l32, key j of register r), both heads
-  float bias[2][16];
   // interior mask bits for pixel parity 0 / 1: register r allowed iff query and key cell are anchors
   uint32_t kbits[2] = {0u, 0u}, jbits = 0u;
   bool qok[2];
-  int ridx[16];  // the 16 index loads in flight together, then the 32 table loads
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
-    ridx[r] = (lvalid && j < 25) ? P.rel_index[l32 * 25 + j] : -1;
-  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
     const int jy = j / 5, jx = j - 5 * (j / 5);
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) bias[hh][r] = ridx[r] >= 0 ? P.rel_table[ridx[r] * 2 + hh] : 0.0f;
     if (j < 25) {
       jbits |= 1u << r;
       kbits[(jy + jx + 1) & 1] |= 1u << r;  // (par + jy + jx) odd
@@ -317,18 +315,6 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
     const int qcell = lvalid ? cy * LP_LW + lx + cx : LP_NCELL;
     const int par = (py + px) & 1;
     const bool interior = py >= 2 && py < H - 2 && px >= 2 && px < W - 2;  // wave-uniform
-    floatx16 sacc[2], oacc[2];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      // S^T = K Q^T over the 16 head dims (lane half h holds dims 8h .. 8h+7)
-      const _Float16* kp = sm + ((1 * 2 + hh) * 2) * QKP + qcell * 16 + 8 * h;
-      const _Float16* qp = sm + ((0 * 2 + hh) * 2) * QKP + qcell * 16 + 8 * h;
-      const half8 kh_ = *reinterpret_cast<const half8*>(kp), kl_ = *reinterpret_cast<const half8*>(kp + QKP);
-      const half8 qh_ = *reinterpret_cast<const half8*>(qp), ql_ = *reinterpret_cast<const half8*>(qp + QKP);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[hh][r] = 0.0f;
-      sacc[hh] = mfma3(kh_, kl_, qh_, ql_, sacc[hh]);
-    }
     // allowed(r): interior = parity bits; border = the in-image tests of the reference's unfold
     uint32_t allow;
     if (interior) {
@@ -346,27 +332,39 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
         allow |= (qa && ka && j < 25) ? (1u << r) : 0u;
       }
     }
+    _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + (int64_t)py * W + px) * 64;
+    // one head at a time, start to store: only one S and one O accumulator live (<= 128 VGPRs, so
+    // two workgroups share a CU and one's staging overlaps the other's products)
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
+      // S^T = K Q^T over the 16 head dims (lane half h holds dims 8h .. 8h+7)
+      const _Float16* kp = sm + ((1 * 2 + hh) * 2) * QKP + qcell * 16 + 8 * h;
+      const _Float16* qp = sm + ((0 * 2 + hh) * 2) * QKP + qcell * 16 + 8 * h;
+      const half8 kh_ = *reinterpret_cast<const half8*>(kp), kl_ = *reinterpret_cast<const half8*>(kp + QKP);
+      const half8 qh_ = *reinterpret_cast<const half8*>(qp), ql_ = *reinterpret_cast<const half8*>(qp + QKP);
+      floatx16 sacc, oacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.0f;
+      sacc = mfma3(kh_, kl_, qh_, ql_, sacc);
       float mx = -3.0e38f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float v = sacc[hh][r] + bias[hh][r] + (((allow >> r) & 1u) ? 0.0f : -100.0f);
-        sacc[hh][r] = ((jbits >> r) & 1u) ? v : -3.0e38f;
-        mx = fmaxf(mx, sacc[hh][r]);
+        const float v = sacc[r] + sbias[(hh * 16 + r) * 64 + lane] + (((allow >> r) & 1u) ? 0.0f : -100.0f);
+        sacc[r] = ((jbits >> r) & 1u) ? v : -3.0e38f;
+        mx = fmaxf(mx, sacc[r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       float sum = 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sacc[hh][r] = ((jbits >> r) & 1u) ? softmax_exp(sacc[hh][r] - mx) : 0.0f;
-        sum += sacc[hh][r];
+        sacc[r] = ((jbits >> r) & 1u) ? softmax_exp(sacc[r] - mx) : 0.0f;
+        sum += sacc[r];
       }
       sum += __shfl_xor(sum, 32);
       const float inv = 1.0f / sum;
       // O^T = V^T P^T (k = keys; P^T registers 8t .. 8t+7 are k-step t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[hh][r] = 0.0f;
+      for (int r = 0; r < 16; ++r) oacc[r] = 0.0f;
       const _Float16* vh_p = sm + QK_H + (hh * 16 + vrow) * LP_NCP;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -374,28 +372,24 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
         half8 vh, vl;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          pv[e] = sacc[hh][8 * t + e] * inv;
+          pv[e] = sacc[8 * t + e] * inv;
           const int c = voff[t][e] >= 0 ? voff[t][e] + lx : LP_NCELL;
           vh[e] = vh_p[c];
           vl[e] = vh_p[VP + c];
         }
         half8 ph, pl_;
         split8(pv, ph, pl_);
-        oacc[hh] = mfma3(vh, vl, ph, pl_, oacc[hh]);
+        oacc = mfma3(vh, vl, ph, pl_, oacc);
       }
-    }
-    // O^T[d][i]: registers 0..3 are d = 4h .. 4h+3, registers 4..7 are d = 8 + 4h .. +3 of query i
-    if (lvalid) {
-      typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-      _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + (int64_t)py * W + px) * 64;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
+      // O^T[d][i]: registers 0..3 are d = 4h .. 4h+3, registers 4..7 are d = 8 + 4h .. +3 of query i
+      if (lvalid) {
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
           half4 hi, lo;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float v = oacc[hh][4 * g + e];
+            const float v = oacc[4 * g + e];
             const _Float16 hv = (_Float16)v;
             hi[e] = hv;
             lo[e] = (_Float16)(v - (float)hv);
@@ -404,6 +398,7 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_packed_kernel(LocalAttn
           *reinterpret_cast<half4*>(dst + k) = hi;
           *reinterpret_cast<half4*>(dst + 32 + k) = lo;
         }
+      }
     }
   }
 }
