@@ -230,7 +230,7 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                                                                      int npos) {
   constexpr int QKP = LP_NCP * 16;       // halves per (tensor, head, hi|lo) plane
   constexpr int QK_H = 2 * 2 * 2 * QKP;  // q, k x heads x hi|lo
-  constexpr int VP = 32 * LP_NCP;        // halves per v plane (hi or lo)
+  constexpr int VP = 32 * LP_NCP;        // v as (hi, lo) half pairs, one 32-bit word per (channel, cell)
   __shared__ __attribute__((aligned(16))) _Float16 sm[QK_H + 2 * VP];
   // relative-position bias of (query l32, key j of register r), per lane: [head][r][lane] (8 KB;
   // held in registers it pushed the kernel past 128 VGPRs, i.e. one workgroup per CU)
@@ -273,8 +273,8 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       dst[0] = hv;
       dst[QKP] = lv;
     } else {
-      sm[QK_H + (hh * 16 + d) * LP_NCP + cell] = hv;
-      sm[QK_H + VP + (hh * 16 + d) * LP_NCP + cell] = lv;
+      reinterpret_cast<uint32_t*>(sm + QK_H)[(hh * 16 + d) * LP_NCP + cell] =
+          (uint32_t)__builtin_bit_cast(uint16_t, hv) | ((uint32_t)__builtin_bit_cast(uint16_t, lv) << 16);
     }
   }
   __syncthreads();
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       // O^T = V^T P^T (k = keys; P^T registers 8t .. 8t+7 are k-step t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[r] = 0.0f;
-      const _Float16* vh_p = sm + QK_H + (hh * 16 + vrow) * LP_NCP;
+      const uint32_t* vp_p = reinterpret_cast<const uint32_t*>(sm + QK_H) + (hh * 16 + vrow) * LP_NCP;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         float pv[8];
@@ -374,8 +374,9 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         for (int e = 0; e < 8; ++e) {
           pv[e] = sacc[8 * t + e] * inv;
           const int c = voff[t][e] >= 0 ? voff[t][e] + lx : LP_NCELL;
-          vh[e] = vh_p[c];
-          vl[e] = vh_p[VP + c];
+          const uint32_t hl = vp_p[c];  // one read for both halves
+          vh[e] = __builtin_bit_cast(_Float16, (uint16_t)(hl & 0xffffu));
+          vl[e] = __builtin_bit_cast(_Float16, (uint16_t)(hl >> 16));
         }
         half8 ph, pl_;
         split8(pv, ph, pl_);
