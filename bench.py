@@ -134,6 +134,9 @@ def parse(argv=None):
     ap.add_argument("--phase", choices=["both", "decode"], default="both",
                     help="both: a step = compress + decompress (the metric's enc+dec); decode: a step = "
                          "decompress() of streams encoded before the timed region (north_star's decode target)")
+    ap.add_argument("--no-decode-record", action="store_true",
+                    help="phase both: skip the decode sub-record (a second timed region of K decompress-only "
+                         "steps over the streams the timed enc+dec steps produced, with its own roofline)")
     a = ap.parse_args(argv)
     wl = WORKLOADS[a.config]
     a.lanes_auto = a.lanes <= 0 and "MLIC_LANES" not in os.environ and "lanes_many" in wl
@@ -270,6 +273,7 @@ def cpu_baseline(model: str, rate, H: int, W: int, level: int = -1, phase: str =
              "psnr": ref.psnr_uint8(x, x_hat), "H": H, "W": W}
     what = "decoder network + native rANS decode" if phase == "decode" else "encoder+decoder networks + native rANS"
     rec = {"value": round(1.0 / dt, 5), "unit": "images/sec (decode)" if phase == "decode" else "images/sec (enc+dec)",
+           "decode_value": round(1.0 / (t2 - t1), 5),
            "cores": threads, "threads_used": threads, "cores_total": total, "cores_affinity": aff,
            "thread_probe_s": probe_s, "kind": "port",
            "sample": f"1 image {W}x{H} {model} (rate set {rate}, seed {seed}: a GPU job's image): oracle torch-CPU fp32 {what}, "
@@ -403,6 +407,7 @@ def main(argv=None):
     split = {"compress": 0.0, "decompress": 0.0}
     last = {}
     decode_only = a.phase == "decode"
+    mode = {"decode": decode_only}  # run_group's phase: the decode sub-record flips it after the main region
 
     def group_kw(gi):
         return {"stage": 2, "s": [j.level for j in groups[gi][1]]} if is_vbr else {}
@@ -421,7 +426,7 @@ def main(argv=None):
         kw = group_kw(gi)
         with torch.cuda.stream(streams[gi]):
             t_a = time.perf_counter()
-            c = pre[gi] if decode_only else net.compress(xs[gi], **kw)
+            c = pre[gi] if mode["decode"] else net.compress(xs[gi], **kw)
             t_b = time.perf_counter()
             d = net.decompress(c["strings"], c["shape"], **kw)
             t_c = time.perf_counter()
@@ -514,6 +519,28 @@ def main(argv=None):
         roofline, prof = profile_roofline(a, gnet, groups, xs, is_vbr, elapsed / a.steps, dev,
                                           pre=pre if decode_only else None)
 
+    # decode sub-record (phase both): north_star states its target for MLICPP_L DECODE, so the default line
+    # also times decompress() alone -- K more steps over the streams the timed enc+dec steps produced (the
+    # last step's compress() of every request stream), the same request streams and lanes, its own barrier-
+    # bracketed region and max over ranks, its own isolated-pass roofline (encoder launches dropped); the
+    # decoded x_hat must equal the timed steps' bit for bit
+    decode_rec = None
+    if not decode_only and not a.no_decode_record:
+        enc_last = {gi: last[gi] for gi in range(len(groups))}
+        pre.update({gi: enc_last[gi][0] for gi in range(len(groups))})
+        mode["decode"] = True
+        run_steps(1)  # warmup: the decode-only schedule
+        torch.cuda.synchronize()
+        elapsed_d = timed_steps(run_steps, a.steps, distributed, dev, sync=torch.cuda.synchronize)
+        same = all(torch.equal(last[gi][1]["x_hat"], enc_last[gi][1]["x_hat"]) for gi in range(len(groups)))
+        assert same, "decode sub-record: decompress of the timed streams != the timed steps' x_hat"
+        rd = None
+        if not a.no_roofline:
+            rd, _ = profile_roofline(a, gnet, groups, xs, is_vbr, elapsed_d / a.steps, dev, pre=pre,
+                                     write_layers=False)
+        mode["decode"] = False
+        decode_rec = {"elapsed_s": elapsed_d, "roofline": rd, "x_hat_equals_timed_steps": same}
+
     if rank == 0:
         if emulated:  # this rank's images only: a per-GPU prediction
             images = len(jobs) * a.steps
@@ -573,6 +600,17 @@ def main(argv=None):
             "batches_per_step": [len(js) for _, js in groups],
             "quality": quality,
         }
+        if decode_rec is not None:
+            rd = decode_rec["roofline"]
+            out["decode"] = {
+                "metric": "images/sec (decode only: decompress() of the timed enc+dec steps' own streams)",
+                "value": round(images / decode_rec["elapsed_s"], 4), "unit": "images/sec",
+                "ms_per_step": round(1000 * decode_rec["elapsed_s"] / a.steps, 3), "steps": a.steps, "warmup": 1,
+                "step_frac": rd["step_frac"] if rd else None,
+                "x_hat_equals_timed_steps": decode_rec["x_hat_equals_timed_steps"],
+                "roofline": ({k: rd[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
+                                                  "launches_isolated", "avg_launch_us", "step_t_roof_ms", "step_ms",
+                                                  "step_frac", "share_of_isolated_gpu_time")} if rd else None)}
         if emulated:
             out["emulated"] = {"world": a.emulate_world, "rank": a.emulate_rank, "host_cores": len(cores),
                                "note": "one rank's job list of a W-GPU run on one GPU with 1/W of the host cores; "
@@ -584,6 +622,11 @@ def main(argv=None):
             j0 = next((j for j in jobs if j.H * j.W <= 1088 * 1920), jobs[0])
             out["cpu_baseline"], coded = cpu_baseline(j0.model, j0.rate, min(j0.H, 1088), min(j0.W, 1920),
                                                       j0.level if is_vbr else -1, phase=a.phase, seed=j0.seed)
+            if "decode" in out:  # the same oracle run's decoder-side time (decoder network + native rANS decode)
+                out["decode"]["cpu_baseline"] = {"value": out["cpu_baseline"]["decode_value"],
+                                                 "unit": "images/sec (decode)",
+                                                 "cores": out["cpu_baseline"]["cores"], "kind": "port",
+                                                 "sample": "the enc+dec cpu_baseline's image, its decoder half"}
             g0 = q[q[:, F["job"]] == j0.id][0]
             if (coded["H"], coded["W"]) == (j0.H, j0.W):
                 d_lik = float(g0[F["bpp_lik"]]) - coded["bpp_lik"]
@@ -615,7 +658,7 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev, pre=None):
+def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev, pre=None, write_layers=True):
     """pre: the decode phase's pre-encoded streams per group (only decompress launches are counted)."""
     from mlic_amd import _lib
     ncat = C.c_int()
@@ -682,7 +725,7 @@ def profile_roofline(a, gnet, groups, xs, is_vbr, t_step_s, dev, pre=None):
     # --batch 8 --split 1 under rocprofv3 profiles the same launches)
     share = min(8, len(groups[0][1]))
     fam1, layer_rows1 = profile_pass(1, share)
-    if a.layers_out and int(os.environ.get("RANK", "0")) == 0:
+    if write_layers and a.layers_out and int(os.environ.get("RANK", "0")) == 0:
         with open(a.layers_out, "w") as f:  # isolated launches: the per-layer efficiency table
             f.write("\n".join(layer_rows1) + "\n")
 

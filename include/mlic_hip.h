@@ -105,10 +105,12 @@ int mlic_set_poison(mlic_model* m, int on);
  * 3x3 / 5x5 convs (default off, $MLIC_X4_SPLITK=1) -- set it before a handle's first call (the
  * workspace is sized for the setting in force then); "dwpw2" = the form of the fused depthwise +
  * pointwise for Cin = Cout in {96, 128, 160, 192} (-1 default = $MLIC_DWPW2 or 2: the register-row
- * dwpw3_kernel; 1 the row-pipelined LDS form; 0 the round-4 dwpw_kernel) -- every form gives the same
- * bits; "pw3" = the full-resolution 1x1 convs with Cin = Cout (GDN / IGDN at 544 x 960) on that kernel's
- * pointwise form (-1 default = $MLIC_PW3 or 1: from 256 K px per image; 2: every grid; 0 = pw_resident,
- * the same bits) */
+ * dwpw3_kernel; 1 the row-pipelined LDS form, A/B-only library since round 6; 0 the round-4 dwpw_kernel) --
+ * every form gives the same bits; "pw3" = the full-resolution 1x1 convs with Cin = Cout (GDN / IGDN at
+ * 544 x 960) on that kernel's pointwise form (-1 default = $MLIC_PW3 or 1: from 256 K px per image; 2: every
+ * grid; 0 = pw_resident, the same bits); "narrow_limit" = L: coder symbols outside [-L - 1, L] cross PCIe
+ * as int32 (the encoder's overflow copy, the decoder's int32 re-decode) -- a test knob for those fallback
+ * paths, bitstreams unchanged (L <= 0: the int16 range, the default) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
  * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the
@@ -184,6 +186,15 @@ int mlic_rans_encode(const int32_t* symbols, const int32_t* indexes, int64_t n, 
                      size_t cap, size_t* written);
 int mlic_rans_decode(const uint8_t* data, size_t nbytes, const int32_t* indexes, int64_t n, const int32_t* cdf,
                      const int32_t* cdf_len, const int32_t* offset, int n_tables, int stride, int32_t* out);
+/* The decompress path's narrow decode, on the host alone (tests): the stream is decoded in `nparts`
+ * consecutive pieces of n / nparts symbols (the 20 phases of one image) with uint8 table indexes, each
+ * piece first into int16 and, when a value falls outside the narrow range (int16, or
+ * mlic_set_kernel_option("narrow_limit", L)), reset to the piece's start and decoded again into int32 --
+ * exactly PhaseDecoder::run's per-image step.  out: all n symbols as int32; *widened: pieces that
+ * took the int32 fallback. */
+int mlic_rans_decode_narrow(const uint8_t* data, size_t nbytes, const uint8_t* indexes, int64_t n, int nparts,
+                            const int32_t* cdf, const int32_t* cdf_len, const int32_t* offset, int n_tables,
+                            int stride, int32_t* out, int* widened);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,7 @@ def _sig(lib):
         "mlic_pmf_to_quantized_cdf": [p, i, i, p],
         "mlic_rans_encode": [p, p, i64, p, p, p, i, i, p, sz, P(sz)],
         "mlic_rans_decode": [p, sz, p, i64, p, p, p, i, i, p],
+        "mlic_rans_decode_narrow": [p, sz, p, i64, i, p, p, p, i, i, p, P(i)],
     }
     for name, args in sigs.items():
         fn = getattr(lib, name)

@@ -1,6 +1,7 @@
 // Stand-ins for the A/B-only kernel families (ab/*.hip) in the product build (make AB=0, the
 // default): the product never selects them; an explicit request (mlic_set_precision(1), $MLIC_X4=0 with a
-// 5x5 conv, $MLIC_LOCAL_ATTN_VALU=1, mlic_conv_run impl 1 / 6, mlic_local_attn_run impl 0) fails loudly.
+// 5x5 conv, $MLIC_LOCAL_ATTN_VALU=1, mlic_conv_run impl 1 / 6, mlic_local_attn_run impl 0, dwpw2 form 1) fails
+// loudly.
 #include "../kernels.h"
 
 namespace mlic {
@@ -18,5 +19,10 @@ void conv_halo_forward(const ConvParams&, const _Float16*, const _Float16*, int,
   ab_missing("conv_halo");
 }
 void local_attn_valu(const LocalAttnParams&, hipStream_t) { ab_missing("the VALU local attention"); }
+bool dwpw2_lds_ok(const ConvParams&, int) { return false; }
+void dwpw2_lds_forward(const ConvParams&, const _Float16*, const _Float16*, int, const float*, const float*,
+                       hipStream_t) {
+  ab_missing("dwpw2 (the row-pipelined LDS form, mlic_set_kernel_option(\"dwpw2\", 1))");
+}
 
 }  // namespace mlic

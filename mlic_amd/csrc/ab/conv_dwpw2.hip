@@ -32,8 +32,8 @@
 // sources), two A images [k-step][hi / lo][32 pixels x 32 bytes] (the 16-byte halves of pixel row n
 // swapped when (n >> 3) & 1: conflict-free ds_read_b128), taps, bias: 120.6 KB at N = 192.
 // Needs W % 4 == 0 (16-byte pieces, dwordx4 stores), Cin = Cout = N in {96, 128, 160, 192}.
-#include "common.h"
-#include "kernels.h"
+#include "../common.h"
+#include "../kernels.h"
 
 #include <cstdlib>
 
@@ -439,15 +439,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw2_kernel(ConvParams P, int R,
   range_report(P.rflag, bad);
 }
 
-static int d2_num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return n;
-}
+static int d2_num_cus() { return device_cu_count(); }
 
 static int d2_mode(const ConvParams& P) {
   const int e = P.epi & ~EPI_RES;
@@ -456,31 +448,14 @@ static int d2_mode(const ConvParams& P) {
   return -1;
 }
 
-// $MLIC_DWPW2=1 or mlic_set_kernel_option("dwpw2", 1): this form where it applies (A/B switch; default
-// off until it measures faster than dwpw_kernel, profiles/r05/ab/dwpw2_*.log)
-static int g_dwpw2 = -1;
-void dwpw2_set(int on) { g_dwpw2 = on; }
-// the form chosen: 0 = dwpw_kernel, 1 = dwpw2_kernel, 2 = dwpw3_kernel (conv_dwpw3.hip, the default: 8 x 192
-// x 544 x 960 bias / GELU / GELU + residual 1.85 / 2.01 / 2.15 ms against dwpw_kernel's 2.31 / 2.45 / 2.98,
-// profiles/r05/ab/dwpw3_ab.log)
-static int d2_form() {
-  static const int env = [] {
-    const char* e = std::getenv("MLIC_DWPW2");
-    return e ? std::atoi(e) : 2;
-  }();
-  return g_dwpw2 < 0 ? env : g_dwpw2;
-}
-static bool d2_enabled() { return d2_form() == 1; }
-
 // rows per strip: about 32, evened out over the image height
 static int d2_rows(int H) {
   const int n = std::max(1, (H + 16) / 32);
   return (H + n - 1) / n;
 }
 
-bool dwpw2_ok(const ConvParams& P, int cin_pad) {
-  if (d2_form() == 2) return dwpw3_shape_ok(P, cin_pad);
-  if (!d2_enabled()) return false;
+// the A/B arm 1 of mlic_set_kernel_option("dwpw2") (the form selection is in conv_dwpw3.hip)
+bool dwpw2_lds_ok(const ConvParams& P, int cin_pad) {
   if (P.K != 1 || P.stride != 1 || P.pad != 0 || P.nseg != 1 || P.seg[0].C != P.Cin || cin_pad < P.Cin) return false;
   if (P.Cin != P.Cout || (P.Cin != 96 && P.Cin != 128 && P.Cin != 160 && P.Cin != 192)) return false;
   if (d2_mode(P) < 0) return false;
@@ -500,10 +475,9 @@ static void launch_dwpw2(const ConvParams& P, const _Float16* wh, const _Float16
   HIP_OK(hipGetLastError());
 }
 
-void dwpw2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
-                   const float* dwb, hipStream_t st) {
-  if (d2_form() == 2) return dwpw3_forward(P, wh, wl, cin_pad, dww, dwb, st);
-  MLIC_CHECK(dwpw2_ok(P, cin_pad) && dww, "dwpw2: unsupported shape");
+void dwpw2_lds_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                       const float* dwb, hipStream_t st) {
+  MLIC_CHECK(dwpw2_lds_ok(P, cin_pad) && dww, "dwpw2: unsupported shape");
   const int mode = d2_mode(P), res = (P.epi & EPI_RES) ? 1 : 0;
 #define D2_RUN(NN)                                                                               \
   if (P.Cin == NN) {                                                                             \

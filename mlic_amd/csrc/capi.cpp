@@ -233,6 +233,7 @@ int mlic_set_kernel_option(const char* name, int value) {
     else if (n == "x4_splitk") x4_set_splitk(value);
     else if (n == "dwpw2") dwpw2_set(value);
     else if (n == "pw3") pw3_set(value);
+    else if (n == "narrow_limit") set_narrow_limit(value);
     else throw Error("mlic: unknown kernel option " + n);
   });
 }
@@ -633,6 +634,26 @@ int mlic_rans_decode(const uint8_t* data, size_t nbytes, const int32_t* indexes,
     RansDecoderState d;
     d.set_stream(data, nbytes);
     d.decode(indexes, n, t, out);
+  });
+}
+
+int mlic_rans_decode_narrow(const uint8_t* data, size_t nbytes, const uint8_t* indexes, int64_t n, int nparts,
+                            const int32_t* cdf, const int32_t* cdf_len, const int32_t* offset, int n_tables,
+                            int stride, int32_t* out, int* widened) {
+  return guard([&] {
+    MLIC_CHECK(nparts >= 1 && n % nparts == 0 && widened, "rans_decode_narrow: n / nparts");
+    CdfTables t = make_tables(cdf, cdf_len, offset, n_tables, stride);
+    RansDecoderState d;
+    d.set_stream(data, nbytes);
+    const int64_t np = n / nparts;
+    std::vector<int16_t> s16(np);
+    *widened = 0;
+    for (int k = 0; k < nparts; ++k) {
+      if (rans_decode_piece(d, indexes + k * np, np, t, s16.data(), out + k * np))
+        for (int64_t i = 0; i < np; ++i) out[k * np + i] = s16[i];
+      else
+        ++*widened;
+    }
   });
 }
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <stdexcept>
@@ -285,6 +286,23 @@ __device__ __forceinline__ void conv_store_shuf4(const ConvParams& P, int b, int
     a[0] = r.x + a[0]; a[1] = r.y + a[1]; a[2] = r.z + a[2]; a[3] = r.w + a[3];
   }
   *reinterpret_cast<float4*>(P.out + (int64_t)b * P.out_bs + off) = make_float4(a[0], a[1], a[2], a[3]);
+}
+
+// CU count of the CURRENT device (grid sizing of the persistent-style kernels), cached per device id:
+// lane threads of several models may launch on different devices concurrently, so the cache is an
+// array of atomics keyed by hipGetDevice(), not one function static (a racing first store writes the
+// same value)
+inline int device_cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  MLIC_CHECK(dev >= 0 && dev < 64, "device id");
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    cache[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
 }
 
 }  // namespace mlic

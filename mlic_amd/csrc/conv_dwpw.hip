@@ -398,15 +398,7 @@ __global__ __launch_bounds__(DP_THREADS) void dwpw_kernel(ConvParams P, const _F
   range_report(P.rflag, bad);
 }
 
-static int dr_num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return n;
-}
+static int dr_num_cus() { return device_cu_count(); }
 
 // epilogue mode of P (the kernel's MODE), -1 when the kernel has none for it
 static int dw_mode(const ConvParams& P) {

@@ -617,15 +617,7 @@ __global__ __launch_bounds__(N / 16 * 64) void dwpw3_kernel(ConvParams P, int R,
   range_report(P.rflag, bad);
 }
 
-static int d3_num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return n;
-}
+static int d3_num_cus() { return device_cu_count(); }
 
 // rows per strip: the R in 8 .. 34 with the fewest steps for the busiest workgroup, rounds of strips over
 // the CUs x (R + 2 halo rows + ~1 step of strip overhead).  544 x 960 x 8 keeps R = 32 (2040 strips,
@@ -681,6 +673,33 @@ void dwpw3_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, 
   }
   D3_RUN(192) D3_RUN(160) D3_RUN(128) D3_RUN(96)
 #undef D3_RUN
+}
+
+// The fused depthwise + pointwise form for Cin = Cout: $MLIC_DWPW2 / mlic_set_kernel_option("dwpw2"):
+//   2 (default) this register-row kernel (8 x 192 x 544 x 960 bias / GELU / GELU + residual 1.85 / 2.01 /
+//     2.15 ms against dwpw_kernel's 2.31 / 2.45 / 2.98, profiles/r05/ab/dwpw3_ab.log);
+//   0 dwpw_kernel (conv_dwpw.hip, rounds 3-4: one wave per SIMD, the same bits);
+//   1 the row-pipelined LDS form dwpw2_kernel -- an A/B-only family since round 6 (ab/conv_dwpw2.hip,
+//     linked by make AB=1 only: its masked-residual builds gave intermittent wrong rows).
+static int g_dwpw2 = -1;
+void dwpw2_set(int on) { g_dwpw2 = on; }
+static int d2_form() {
+  static const int env = [] {
+    const char* e = std::getenv("MLIC_DWPW2");
+    return e ? std::atoi(e) : 2;
+  }();
+  return g_dwpw2 < 0 ? env : g_dwpw2;
+}
+bool dwpw2_ok(const ConvParams& P, int cin_pad) {
+  const int f = d2_form();
+  if (f == 2) return dwpw3_shape_ok(P, cin_pad);
+  if (f == 1) return dwpw2_lds_ok(P, cin_pad);
+  return false;
+}
+void dwpw2_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                   const float* dwb, hipStream_t st) {
+  if (d2_form() == 2) return dwpw3_forward(P, wh, wl, cin_pad, dww, dwb, st);
+  dwpw2_lds_forward(P, wh, wl, cin_pad, dww, dwb, st);
 }
 
 // the pointwise form (PW) for the full-resolution 1x1 convs with Cin = Cout (pw_resident's MODE 0 - 3: bias,

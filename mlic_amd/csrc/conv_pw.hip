@@ -300,15 +300,7 @@ __global__ __launch_bounds__(PW_THREADS) void pw_resident_kernel(ConvParams P, c
   range_report(P.rflag, bad);
 }
 
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return n;
-}
+static int num_cus() { return device_cu_count(); }
 
 // epilogue mode of P (see the kernel's MODE), -1 when the kernel has none for it
 static int pw_mode(const ConvParams& P) {

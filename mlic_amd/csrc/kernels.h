@@ -48,8 +48,12 @@ bool dwpw_grid_ok(const ConvParams& P);
 // takes the chosen one (dwpw2_set) where it applies
 bool dwpw2_ok(const ConvParams& P, int cin_pad);
 // mlic_set_kernel_option("dwpw2"): -1 = $MLIC_DWPW2 (default 2), 0 = dwpw_kernel, 1 = the row-pipelined
-// LDS form (conv_dwpw2.hip), 2 = the register-row form (conv_dwpw3.hip)
+// LDS form (ab/conv_dwpw2.hip: A/B-only family, make AB=1), 2 = the register-row form (conv_dwpw3.hip)
 void dwpw2_set(int on);
+// the A/B-only row-pipelined LDS form (ab/conv_dwpw2.hip; the product build's stub reports false / throws)
+bool dwpw2_lds_ok(const ConvParams& P, int cin_pad);
+void dwpw2_lds_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, int cin_pad, const float* dww,
+                       const float* dwb, hipStream_t st);
 bool dwpw3_shape_ok(const ConvParams& P, int cin_pad);
 // the same kernel's pointwise-only form for the full-resolution 1x1 convs (pw_resident MODE 0 - 3, Cin = Cout
 // in {96, 128, 160, 192}): pw_resident_forward takes it where pw3_ok; mlic_set_kernel_option("pw3"):
@@ -199,6 +203,7 @@ struct QuantParams {
   int16_t* sym16;
   uint8_t* idx8;
   int* ovf;
+  int nlim;  // the narrow range [-nlim - 1, nlim]: 32767 (int16); smaller only under the test knob below
   const float* table;
   int ntable;
   int phase;  // 0 anchor, 1 non-anchor

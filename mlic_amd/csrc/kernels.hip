@@ -724,8 +724,9 @@ __global__ void quant_phase_kernel(QuantParams P) {
     if (P.sym) P.sym[sq] = (int32_t)q;
     if (P.idx) P.idx[sq] = ix;
     if (P.sym16) {
-      const bool fits = q >= -32768.0f && q <= 32767.0f;
-      P.sym16[sq] = (int16_t)(fits ? q : (q < 0.0f ? -32768.0f : 32767.0f));
+      const float lim = (float)P.nlim;  // 32767 unless a test lowers it (narrow_limit)
+      const bool fits = q >= -lim - 1.0f && q <= lim;
+      P.sym16[sq] = (int16_t)(fits ? q : (q < 0.0f ? -lim - 1.0f : lim));
       P.idx8[sq] = (uint8_t)ix;
       if (!fits) *P.ovf = 1;  // a vector store from the lanes that overflow (benign race: all store 1)
     }

@@ -1192,13 +1192,7 @@ class PhaseDecoder {
     std::vector<char> wide(parts, 0);
     auto work = [&](int b) {
       HostStats::Scope d{hs_->dec_ns};
-      RansDecoderState& dec = dec_[b];
-      const RansDecoderState::Mark m = dec.mark();
-      if (!dec.decode(h_idx8_ + b * n, n, *t_, h_sym16_ + b * n)) {
-        dec.reset(m);
-        dec.decode(h_idx8_ + b * n, n, *t_, h_sym_ + b * n);
-        wide[b] = 1;
-      }
+      if (!rans_decode_piece(dec_[b], h_idx8_ + b * n, n, *t_, h_sym16_ + b * n, h_sym_ + b * n)) wide[b] = 1;
     };
     if (parts == 1) work(0);
     else pool_->run(B, work, HostPool::DECODE);
@@ -1310,6 +1304,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
           Q.sym16 = cb->sym16 + off;
           Q.idx8 = cb->idx8 + off;
           Q.ovf = cb->ovf;
+          Q.nlim = narrow_limit();
         }
         timed(PCAT_ELEM, 0.0, 4.0 * L().B * C * HW * 5, [&] { quant_phase(Q, L().st); }, "quant_phase");
         Lane& l = L();

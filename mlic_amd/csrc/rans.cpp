@@ -7,6 +7,7 @@
 #include "rans.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -154,6 +155,10 @@ uint32_t RansDecoderState::get_word() {
   return pos_ < words_.size() ? words_[pos_++] : 0u;
 }
 
+static std::atomic<int> g_narrow_limit{32767};
+void set_narrow_limit(int lim) { g_narrow_limit.store(lim <= 0 || lim > 32767 ? 32767 : lim); }
+int narrow_limit() { return g_narrow_limit.load(std::memory_order_relaxed); }
+
 template <class I, class S>
 bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S* out) {
   constexpr uint64_t mask = (1ull << PRECISION) - 1;
@@ -163,6 +168,7 @@ bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S
   const uint64_t* lut = t.lut.data();
   const int32_t* cdfs = t.cdf.data();
   const int stride = t.stride;
+  const int32_t nhi = sizeof(S) < sizeof(int32_t) ? (int32_t)narrow_limit() : 0;  // the narrow range
   uint64_t state = state_;
   for (int64_t i = 0; i < n; ++i) {
     const int32_t ci = (int32_t)indexes[i];
@@ -210,7 +216,7 @@ bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S
       else value += max_value;
     }
     const int32_t v = value + off[ci];
-    if (sizeof(S) < sizeof(int32_t) && (v < (int32_t)std::numeric_limits<S>::min() || v > (int32_t)std::numeric_limits<S>::max())) {
+    if (sizeof(S) < sizeof(int32_t) && (v < -nhi - 1 || v > nhi)) {
       state_ = state;  // the caller resets to its mark and decodes again into a wider type
       return false;
     }
@@ -220,6 +226,15 @@ bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S
   return true;
 }
 template bool RansDecoderState::decode<int32_t, int32_t>(const int32_t*, int64_t, const CdfTables&, int32_t*);
+
+bool rans_decode_piece(RansDecoderState& d, const uint8_t* indexes, int64_t n, const CdfTables& t, int16_t* s16,
+                       int32_t* s32) {
+  const RansDecoderState::Mark m = d.mark();
+  if (d.decode(indexes, n, t, s16)) return true;
+  d.reset(m);
+  d.decode(indexes, n, t, s32);
+  return false;
+}
 template bool RansDecoderState::decode<uint8_t, int32_t>(const uint8_t*, int64_t, const CdfTables&, int32_t*);
 template bool RansDecoderState::decode<uint8_t, int16_t>(const uint8_t*, int64_t, const CdfTables&, int16_t*);
 

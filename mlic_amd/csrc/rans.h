@@ -54,6 +54,19 @@ class RansEncoder {
   void grow();
 };
 
+// The narrow-transfer range test knob (mlic_set_kernel_option("narrow_limit", L)): symbols outside
+// [-L - 1, L] take the int32 fallback on both sides (the encoder's *ovf copy, the decoder's re-decode into
+// int32); default / L <= 0 / L > 32767: the int16 range.  Bitstreams are the same bytes whatever L is;
+// the knob exists so that the fallback paths run in tests.
+void set_narrow_limit(int lim);
+int narrow_limit();
+
+class RansDecoderState;
+// one piece (a phase of one image) of the decompress path's narrow decode: into s16 when every value fits
+// the narrow range (returns true), else reset to the piece's start and decoded into s32 (returns false)
+bool rans_decode_piece(RansDecoderState& d, const uint8_t* indexes, int64_t n, const CdfTables& t, int16_t* s16,
+                       int32_t* s32);
+
 class RansDecoderState {
  public:
   void set_stream(const uint8_t* data, size_t nbytes);

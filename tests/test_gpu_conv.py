@@ -404,7 +404,7 @@ def test_depthwise_strip_vs_tile(B, Cn, H, W, gelu):
     (1, 96, 3, 2, 1),        # a single pair: both halo pairs out of the image
     (1, 192, 5, 960, 1),     # full-resolution width
     (2, 128, 8, 184, 64),    # Cin 128, ragged last segment (4 pairs)
-    # the producer / consumer form (conv_dwpw2.hip: Cin = Cout in 96..192, W % 4 == 0)
+    # Cin = Cout in 96..192 (the default register-row form, conv_dwpw3.hip)
     (2, 192, 98, 480, 1 | 64),  # several 6 x 32 tiles per workgroup, ragged row block (98 = 16 x 6 + 2)
     (1, 160, 100, 320, 1),   # N = 160, 5 consumer waves
     (2, 96, 40, 228, 0),     # N = 96, ragged last column tile (228 = 7 x 32 + 4)
@@ -416,17 +416,21 @@ def test_dwpw_fused(B, Cn, H, W, epi):
     _dwpw_case(B, Cn, Cn, H, W, epi)
 
 
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("B,Cn,H,W,epi", [
     (2, 192, 68, 120, 1 | 64), (3, 192, 20, 96, 64), (2, 192, 98, 480, 1 | 64), (1, 160, 100, 320, 1),
     (2, 96, 40, 228, 0), (2, 128, 8, 184, 64), (1, 192, 5, 960, 1), (2, 192, 40, 100, 1),
     (1, 96, 33, 62, 1 | 64), (2, 160, 9, 130, 1), (1, 128, 70, 64, 1 | 64)])
 def test_dwpw2_fused(B, Cn, H, W, epi, form):
-    """The producer / consumer forms (A/B arms of mlic_set_kernel_option("dwpw2", form)): 1 = the
-    row-pipelined LDS form (conv_dwpw2.hip), 2 = the register-row form (conv_dwpw3.hip, 64-pixel strips:
-    ragged, narrower-than-a-strip and exact-multiple widths): the same bits as depthwise + resident
-    pointwise."""
+    """The fused Cin = Cout forms (mlic_set_kernel_option("dwpw2", form)): 0 = dwpw_kernel (conv_dwpw.hip,
+    one wave per SIMD), 1 = the row-pipelined LDS form (ab/conv_dwpw2.hip, A/B-only library), 2 = the
+    register-row form (conv_dwpw3.hip, the default; 64-pixel strips: ragged, narrower-than-a-strip and
+    exact-multiple widths): the same bits as depthwise + resident pointwise.  (2, 192, 68, 120, GELU +
+    residual) and (3, 192, 20, 96, residual) are the shapes on which form 1's masked-residual builds
+    returned wrong rows."""
     from mlic_amd import _lib
+    if form == 1 and not _lib.ab_families():
+        pytest.skip("dwpw2 is an A/B-only kernel family (make AB=1)")
     _lib.call("mlic_set_kernel_option", b"dwpw2", form)
     try:
         _dwpw_case(B, Cn, Cn, H, W, epi)

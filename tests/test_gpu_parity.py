@@ -249,6 +249,33 @@ def test_lanes_do_not_change_bitstreams():
         assert ci["strings"][0][0] == outs[0][0][0][i] and ci["strings"][1][0] == outs[0][0][1][i]
 
 
+@pytest.mark.parametrize("batch_stream", [False, True])
+def test_narrow_transfer_fallback(batch_stream):
+    """the coder inputs cross PCIe as int16 symbols / uint8 indexes, with an int32 fallback
+    for a symbol beyond int16 (encoder: the overflow flag brings the int32 copy; decoder: the phase is
+    decoded again into int32 and the parts that fit are widened beside it).  The "narrow_limit" knob
+    shrinks the narrow range to [-2, 1] so that both fallbacks run on ordinary images: the bytes must
+    equal the default run's and decompress must still equal forward() bit for bit, for per-image streams
+    and for the reference's single batched y stream."""
+    net = net_for("MLICPP_S")
+    net.update()
+    x = torch.cat([synthetic.synth_image(128, 192, 60 + i) for i in range(2)]).to(DEV)
+    xf = net(x)["x_hat"]
+    c0 = net.compress(x, batch_stream=batch_stream)
+    sym = np.concatenate([net.encoded_streams(b)[0] for b in range(2)]) if not batch_stream else None
+    try:
+        _lib.call("mlic_set_kernel_option", b"narrow_limit", 1)
+        c1 = net.compress(x, batch_stream=batch_stream)
+        d1 = net.decompress(c1["strings"], c1["shape"])
+    finally:
+        _lib.call("mlic_set_kernel_option", b"narrow_limit", 0)
+    d0 = net.decompress(c0["strings"], c0["shape"])
+    assert c1["strings"] == c0["strings"]
+    assert torch.equal(d1["x_hat"], d0["x_hat"]) and torch.equal(d0["x_hat"], xf)
+    if sym is not None:  # the knob did force the fallbacks: symbols outside [-2, 1] were coded
+        assert int(((sym > 1) | (sym < -2)).sum()) > 0
+
+
 def test_reference_batched_y_stream(golden):
     """The reference's B > 1 layout (mlicpp.py:215, 279-281 compress, 306-307 decompress): ONE y stream
     for the batch.  compress(batch_stream=True) emits it -- its coder inputs equal the reference's own
@@ -801,6 +828,10 @@ INTEROP = [("forward_MLICPP_L_192x256_r0", "MLICPP_L", 0, None, 3), ("forward_ML
            ("forward_MLICPP_S_VBR_192x256_s1", "MLICPP_S_VBR", None, 1, 3)]
 
 
+# fixtures with a known scale-index bucket flip against the reference, and the bound on it
+INTEROP_FLIP = {"forward_MLICPP_L_128x192": 1, "forward_MLICPP_M_SMALL_DEC_128x128": 1}
+
+
 @pytest.mark.parametrize("fixture,name,rate,s,img", INTEROP)
 def test_reference_coder_lists_decode(golden, fixture, name, rate, s, img):
     """Interop: y / z streams built by the native coder from the REFERENCE's own coder
@@ -840,6 +871,12 @@ def test_reference_coder_lists_decode(golden, fixture, name, rate, s, img):
         rec.update(decode_error=str(e))
         assert not agree, rec
     PARITY[f"interop_{fixture}"] = rec
+    # pinned: the 8 fixtures whose indexes agree today must keep agreeing; the two with one
+    # bucket flip (fp32 summation order) may not drift further
+    if fixture in INTEROP_FLIP:
+        assert rec["y_index_mismatch"] <= INTEROP_FLIP[fixture], rec
+    else:
+        assert agree, rec
     if agree:
         assert rec["bytes_equal_own"], rec
         assert torch.equal(d["x_hat"], f["x_hat"]), rec

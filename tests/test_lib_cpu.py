@@ -146,6 +146,46 @@ def test_rans_bypass_and_extremes(golden, seed):
     assert data == ref
 
 
+def _decode_narrow(data, idx8, nparts, cdf, length, offset):
+    cdf_, length_, offset_ = (np.ascontiguousarray(np.asarray(v), dtype=np.int32) for v in (cdf, length, offset))
+    out = np.zeros(idx8.size, np.int32)
+    widened = C.c_int(-1)
+    _lib.call("mlic_rans_decode_narrow", data, len(data), idx8.ctypes.data, idx8.size, nparts, cdf_.ctypes.data,
+              length_.ctypes.data, offset_.ctypes.data, cdf_.shape[0], cdf_.shape[1], out.ctypes.data,
+              C.byref(widened))
+    return out, widened.value
+
+
+@pytest.mark.parametrize("limit", [0, 40, 3])
+def test_rans_narrow_decode_fallback(golden, limit):
+    """The decompress path's narrow decode: each phase is decoded into int16 and, when a value
+    leaves the narrow range, the decoder resets to the phase's start and decodes it again into int32
+    (PhaseDecoder::run -> rans_decode_piece).  The narrow range is lowered with the "narrow_limit" knob so
+    that the fallback runs here: the symbols must come back exactly, the pieces that widen are exactly the
+    ones holding an out-of-range value, and the stream is consumed in step (later pieces decode right)."""
+    cdf, length, offset = _gc_tables(golden)
+    r = np.random.default_rng(11)
+    nparts, npiece = 20, 750
+    idx8 = r.integers(0, 64, nparts * npiece).astype(np.uint8)
+    sym = (r.standard_normal(nparts * npiece) * 4).astype(np.int32)
+    sym[3 * npiece + 7] = 70000            # beyond int16: piece 3 must widen at every limit
+    sym[8 * npiece + 100] = -40000         # piece 8 too
+    sym[12 * npiece + 5] = 41              # beyond the limit of 40 only
+    data = entropy.rans_encode(sym, idx8.astype(np.int32), cdf, length, offset)
+    try:
+        _lib.call("mlic_set_kernel_option", b"narrow_limit", limit)
+        back, widened = _decode_narrow(data, idx8, nparts, cdf, length, offset)
+    finally:
+        _lib.call("mlic_set_kernel_option", b"narrow_limit", 0)
+    assert np.array_equal(back, sym)
+    lim = 32767 if limit <= 0 else limit
+    want = sum(1 for k in range(nparts) if np.any((sym[k * npiece:(k + 1) * npiece] > lim) |
+                                                  (sym[k * npiece:(k + 1) * npiece] < -lim - 1)))
+    assert widened == want and widened >= 2
+    # the plain int32 decoder agrees on the same stream
+    assert np.array_equal(entropy.rans_decode(data, idx8.astype(np.int32), cdf, length, offset), sym)
+
+
 def test_rans_empty_stream(golden):
     cdf, length, offset = _gc_tables(golden)
     data = entropy.rans_encode(np.zeros(0, np.int32), np.zeros(0, np.int32), cdf, length, offset)
