@@ -40,8 +40,12 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int CH_T = 256;      // threads (4 waves)
 constexpr int CH_BN = 128;     // pixels per workgroup
+// NJ = 16-pixel column blocks per wave: 2 = four waves of 32 pixels (one wave per SIMD, 512-register
+// waves: rounds 2-5), 1 = eight waves of 16 pixels (two waves per SIMD, <= 256 registers each: one wave's
+// bias / GELU / split VALU work runs beside the other's MFMAs instead of in its own MFMA shadow only)
+template <int NJ>
+constexpr int ch_threads() { return 64 * (8 / NJ); }
 
 __device__ __forceinline__ int chswz(int row) { return (row >> 1) & 7; }
 
@@ -69,20 +73,22 @@ __device__ unsigned long long* g_chain_trace;
 constexpr int CH_TR_STEPS = 64;
 #endif
 
-template <int C1, int C2, int C3, int C4>
-__global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
+template <int C1, int C2, int C3, int C4, int NJ>
+__global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) {
+  constexpr int CH_T = ch_threads<NJ>(), NW = CH_T / 64, PW = 16 * NJ;  // threads, waves, pixels per wave
   constexpr int NL = C4 ? 4 : (C3 ? 3 : 2);
   constexpr int WSLOT = C1 * 128;  // layer 0 is the widest (checked by the host side)
   constexpr int B_OFF = 2 * WSLOT;
   constexpr int NB = C1 + C2 + C3 + C4;
-  constexpr int WMAX = C1 / 32;  // 1-KB weight pieces per wave of the widest step
+  constexpr int WMAX = C1 / 32 * 4 / NW;  // 1-KB weight pieces per wave of the widest step
   static_assert(C1 % 32 == 0 && C2 % 32 == 0 && (C3 == 0 || C3 % 32 == 0) && (C4 == 0 || C4 % 16 == 0), "dims");
+  static_assert(NJ == 2 || (C1 % 64 == 0 && C2 % 64 == 0 && C3 % 64 == 0 && C4 % 64 == 0), "8 waves: rows / 64 pieces");
   static_assert(C2 <= C1 && C3 <= C1 && C4 <= C1, "layer 0 is the widest");
   static_assert(B_OFF + NB * 4 <= 160 * 1024, "chain LDS");
   __shared__ __attribute__((aligned(1024))) char sm[B_OFF + NB * 4];
   float* sbias = reinterpret_cast<float*>(sm + B_OFF);
 #ifdef MLIC_CHAIN_TRACE
-  __shared__ unsigned long long str[4][CH_TR_STEPS][3];
+  __shared__ unsigned long long str[NW][CH_TR_STEPS][3];
   const int tr_wg = (blockIdx.x == 0 && blockIdx.y == 0) ? 0
                     : (blockIdx.x == gridDim.x - 2 && blockIdx.y == gridDim.y - 1) ? 1 : -1;
 #define CH_TR(t, k) \
@@ -122,11 +128,11 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     return C4;
   };
 
-  // weights of step u: wave wv moves 1-KB pieces wv*n .. wv*n + n - 1 (n = rows / 32) through wr
+  // weights of step u: wave wv moves 1-KB pieces wv*n .. wv*n + n - 1 (n = rows / 32 / (NW / 4)) through wr
   u32x4 wr[WMAX];
   int64_t w_off = 0;  // halves: the image of the next step to load
   auto wload = [&](int u) {
-    const int R = rows_of(u), n = R / 32;
+    const int R = rows_of(u), n = R / 32 * 4 / NW;
     const _Float16* src = P.wimg + w_off + (int64_t)(wv * n) * 512 + lane * 8;
 #pragma unroll
     for (int i = 0; i < WMAX; ++i)
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     w_off += (int64_t)R * 64;
   };
   auto wstore = [&](int u) {
-    const int n = rows_of(u) / 32;
+    const int n = rows_of(u) / 32 * 4 / NW;
     char* dst = sm + (u & 1) * WSLOT + (wv * n) * 1024 + lane * 16;
 #pragma unroll
     for (int i = 0; i < WMAX; ++i)
@@ -154,18 +160,18 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   };
 
   // layer-0 input, 2 K-steps ahead in registers: lane (G, l16) loads exactly its B fragments,
-  // channels 32t + 8G .. +7 at pixels p0 + 32 wv + 16 j + l16 (16 dword loads; the 32 channels of a
-  // K-step lie in one input segment, segments being multiples of 32).  Every L0 step issues its 16
+  // channels 32t + 8G .. +7 at pixels p0 + PW wv + 16 j + l16 (8 NJ dword loads; the 32 channels of a
+  // K-step lie in one input segment, segments being multiples of 32).  Every L0 step issues its
   // loads (the last two re-load chunk S0 - 1), so the ring's vmcnt stays a plain count.
-  auto load_f = [&](int t, float (&f)[2][8]) {
+  auto load_f = [&](int t, float (&f)[NJ][8]) {
     t = min(t, S0 - 1);
     const int ch = 32 * t;
     int s = 0, c0 = 0;
     while (s + 1 < P.nseg && ch >= c0 + P.seg[s].C) { c0 += P.seg[s].C; ++s; }
     const float* src = P.seg[s].p + (int64_t)b * P.seg[s].bs + (int64_t)(ch - c0 + 8 * G) * HW;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int px = min(p0 + 32 * wv + 16 * j + l16, HW - 1);  // ragged last tile: outputs dropped
+    for (int j = 0; j < NJ; ++j) {
+      const int px = min(p0 + PW * wv + 16 * j + l16, HW - 1);  // ragged last tile: outputs dropped
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HW + px];
     }
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   // one K-step of COUT rows against B operands in registers; the A fragments of row block i + 2 are
   // read while block i's MFMAs issue (12 MFMAs of cover for the LDS latency); hook(i) runs after
   // block i's MFMAs (program-order interleave of independent VALU work)
-  auto kstep = [&](auto& acc, const char* As, const half8 (&bh)[2], const half8 (&bl)[2], auto cout_c, auto&& hook) {
+  auto kstep = [&](auto& acc, const char* As, const half8 (&bh)[NJ], const half8 (&bl)[NJ], auto cout_c, auto&& hook) {
     constexpr int COUT = decltype(cout_c)::value, NBK = COUT / 16, D = 2, R = D + 1;
     half8 ah[R], al[R];
 #pragma unroll
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
         al[(i + D) % R] = chain_frag(As, 16 * (i + D) + l16, G + 4);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) mfma3(acc[i][j], ah[i % R], al[i % R], bh[j], bl[j]);
+      for (int j = 0; j < NJ; ++j) mfma3(acc[i][j], ah[i % R], al[i % R], bh[j], bl[j]);
       hook(i);
     }
   };
@@ -202,14 +208,14 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 
   int bad = 0;  // fp16 range guard (common.h)
   // ------------------------------------------------------------------ layer 0 (input prefetched)
-  floatx4 acc0[C1 / 16][2];
+  floatx4 acc0[C1 / 16][NJ];
   if (P.aux) {
     // the hoisted part of layer 0 (EntropyParameters' hyper columns, one wide GEMM per image) starts
     // the accumulators, in the prescaled domain of this layer's weights (exact)
     const float* ax = P.aux + (int64_t)b * P.aux_bs;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int px = min(p0 + 32 * wv + 16 * j + l16, HW - 1);
+    for (int j = 0; j < NJ; ++j) {
+      const int px = min(p0 + PW * wv + 16 * j + l16, HW - 1);
 #pragma unroll
       for (int i = 0; i < C1 / 16; ++i)
 #pragma unroll
@@ -218,13 +224,13 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   } else {
 #pragma unroll
     for (int i = 0; i < C1 / 16; ++i)
-      for (int j = 0; j < 2; ++j) acc0[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc0[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
-  auto step0 = [&](int t, float (&f)[2][8]) {
+  auto step0 = [&](int t, float (&f)[NJ][8]) {
     step_begin(t);
-    half8 bh[2], bl[2];
+    half8 bh[NJ], bl[NJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) split8(f[j], bh[j], bl[j]);
+    for (int j = 0; j < NJ; ++j) split8(f[j], bh[j], bl[j]);
     // keep the reload of f below its last use, so the ring slot stays in the same registers (an
     // overlap would make the register allocator rotate the ring with copies that wait for the loads)
     __builtin_amdgcn_sched_barrier(0);
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   wstore(0);
   if (T > 1) wload(1);
   if (S0 > 0) {
-    float fa[2][8], fb[2][8];
+    float fa[NJ][8], fb[NJ][8];
     load_f(0, fa);
     load_f(1, fb);
     int t = 0;
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   // K-chunk c of a layer's accumulators -> the next layer's B operands (bias + GELU + split, in
   // registers; 2^-wexp is exact, so the fma equals ldexp + add), one value pair at a time: pair pi =
   // (j = pi >> 2, q = (pi >> 1) & 1, e = 2 (pi & 1)); the split of column block j follows its 4th pair
-  auto chunk_pair = [&](auto& acc, int c, int pi, float (&v)[2][8], half8 (&oh)[2], half8 (&ol)[2], int boff,
+  auto chunk_pair = [&](auto& acc, int c, int pi, float (&v)[NJ][8], half8 (&oh)[NJ], half8 (&ol)[NJ], int boff,
                         float unscale) {
     const int j = pi >> 2, q = (pi >> 1) & 1, e = 2 * (pi & 1);
     const float* bq = sbias + boff + 32 * c + 16 * q + 4 * G + e;
@@ -278,20 +284,26 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
   // independent of those MFMAs); chunk 0's before the first step.
   auto layer_regs = [&](auto& acc, auto& prev, auto nch_c, auto cout_c, int t0, int boff, int wexp) {
     constexpr int NCH = decltype(nch_c)::value, COUT = decltype(cout_c)::value, NBK = COUT / 16;
-    constexpr int PER = NBK >= 8 ? NBK / 8 : 1, PPB = NBK >= 8 ? 1 : 8 / NBK;  // blocks per pair, pairs per block
+    constexpr int NP = 4 * NJ;  // value pairs of a K-chunk per lane
+    constexpr int PER = NBK >= NP ? NBK / NP : 1, PPB = NBK >= NP ? 1 : NP / NBK;  // blocks per pair, pairs per block
     const float unscale = ldexpf(1.0f, -wexp);
 #pragma unroll
     for (int i = 0; i < COUT / 16; ++i)
-      for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    half8 nh[2], nl[2];
-    float v[2][8];
+      for (int j = 0; j < NJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    half8 nh[NJ], nl[NJ];
+    float v[NJ][8];
 #pragma unroll
-    for (int pi = 0; pi < 8; ++pi) chunk_pair(prev, 0, pi, v, nh, nl, boff, unscale);
+    for (int pi = 0; pi < NP; ++pi) chunk_pair(prev, 0, pi, v, nh, nl, boff, unscale);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int t = t0 + c;
       step_begin(t);
-      const half8 b_h[2] = {nh[0], nh[1]}, b_l[2] = {nl[0], nl[1]};
+      half8 b_h[NJ], b_l[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        b_h[j] = nh[j];
+        b_l[j] = nl[j];
+      }
       kstep(acc, sm + (t & 1) * WSLOT, b_h, b_l, cout_c, [&](int i) {
         if (c + 1 < NCH && i % PER == 0)
 #pragma unroll
@@ -313,8 +325,8 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
 #pragma unroll
     for (int i = 0; i < COUT / 16; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int px = p0 + 32 * wv + 16 * j + l16;
+      for (int j = 0; j < NJ; ++j) {
+        const int px = p0 + PW * wv + 16 * j + l16;
         if (px >= HW) continue;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -328,17 +340,17 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(ChainParams P) {
     range_report(P.rflag, bad != 0);
   };
 
-  floatx4 acc1[C2 / 16][2];
+  floatx4 acc1[C2 / 16][NJ];
   layer_regs(acc1, acc0, I1{}, std::integral_constant<int, C2>{}, S0, 0, P.wexp[0]);
   if constexpr (NL == 2) {
     store(acc1, std::integral_constant<int, C2>{}, C1, P.wexp[1]);
   } else {
-    floatx4 acc2[C3 / 16][2];
+    floatx4 acc2[C3 / 16][NJ];
     layer_regs(acc2, acc1, I2{}, std::integral_constant<int, C3>{}, S0 + S1, C1, P.wexp[1]);
     if constexpr (NL == 3) {
       store(acc2, std::integral_constant<int, C3>{}, C1 + C2, P.wexp[2]);
     } else {
-      floatx4 acc3[C4 / 16][2];
+      floatx4 acc3[C4 / 16][NJ];
       layer_regs(acc3, acc2, I3{}, std::integral_constant<int, C4>{}, S0 + S1 + S2, C1 + C2, P.wexp[2]);
       store(acc3, std::integral_constant<int, C4>{}, C1 + C2 + C3, P.wexp[3]);
     }
@@ -380,18 +392,39 @@ bool chain_supported(int nl, const int* cout) {
   return false;
 }
 
+// $MLIC_CHAIN_NJ / mlic_set_kernel_option("chain_nj"): 16-pixel column blocks per wave (1: eight waves
+// of 16 pixels, 2: four waves of 32); the same MFMA order per accumulator and the same K order, so both
+// give the same bits
+static int g_chain_nj = -1;
+void chain_set_nj(int nj) { g_chain_nj = nj; }
+static int chain_nj() {
+  static const int env = [] {
+    const char* e = std::getenv("MLIC_CHAIN_NJ");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int v = g_chain_nj > 0 ? g_chain_nj : env;
+  return v == 2 ? 2 : 1;
+}
+
+template <int NJ>
+static void launch_chain(const ChainParams& P, int nl, const int* cout, hipStream_t st) {
+  dim3 grid((P.HW + CH_BN - 1) / CH_BN, P.B);
+  constexpr int T = ch_threads<NJ>();
+  if (nl == 4 && cout[3] == 64)
+    hipLaunchKernelGGL((chain_kernel<320, 256, 128, 64, NJ>), grid, dim3(T), 0, st, P);
+  else if (nl == 4)
+    hipLaunchKernelGGL((chain_kernel<320, 256, 128, 128, NJ>), grid, dim3(T), 0, st, P);
+  else
+    hipLaunchKernelGGL((chain_kernel<128, 64, 0, 0, NJ>), grid, dim3(T), 0, st, P);
+  HIP_OK(hipGetLastError());
+}
+
 void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st) {
   MLIC_CHECK(chain_supported(nl, cout), "chain: unsupported layer widths");
   MLIC_CHECK(P.cin0 % 64 == 0 && (P.cin0 > 0 || P.aux) && P.HW % 4 == 0 && P.HW >= 4,
              "chain: Cin multiple of 64 (or 0 with aux), HW of 4");
-  dim3 grid((P.HW + CH_BN - 1) / CH_BN, P.B);
-  if (nl == 4 && cout[3] == 64)
-    hipLaunchKernelGGL((chain_kernel<320, 256, 128, 64>), grid, dim3(CH_T), 0, st, P);
-  else if (nl == 4)
-    hipLaunchKernelGGL((chain_kernel<320, 256, 128, 128>), grid, dim3(CH_T), 0, st, P);
-  else
-    hipLaunchKernelGGL((chain_kernel<128, 64, 0, 0>), grid, dim3(CH_T), 0, st, P);
-  HIP_OK(hipGetLastError());
+  if (chain_nj() == 2) launch_chain<2>(P, nl, cout, st);
+  else launch_chain<1>(P, nl, cout, st);
 }
 
 }  // namespace mlic

@@ -72,6 +72,12 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 // every tap reads its fragments from that image at the tap's (ky, kx) shift -- instead of 256 lines
 // per tap (K^2 x the L2 -> LDS bytes and VMEM instructions for B).  The next chunk's halo is loaded one
 // piece per thread per step, spread over the current chunk's taps, into the other halo slot.
+// diagnostics builds only (-DMLIC_X4_ABL_RS=mask, never the product): 1 = no staging in the K loop
+// (the prologue's LDS images are re-read every step), 2 = no MFMAs (fragment reads kept alive), 4 = no
+// per-step barrier -- wrong results, timing decomposition of the register-staged loop
+#ifndef MLIC_X4_ABL_RS
+#define MLIC_X4_ABL_RS 0
+#endif
 template <int K, int BM, bool RS, bool HI, bool DIR = false, bool HALO = false>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
                                                       const _Float16* __restrict__ wx, int nchunk, int H, int W,
@@ -316,7 +322,12 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           bh[(j + 1) & 1] = lds_frag(Bs, n, G);
           bl[(j + 1) & 1] = lds_frag(Bs, n, G + 4);
         }
-        if constexpr (HI) {
+        if constexpr ((MLIC_X4_ABL_RS & 2) != 0) {
+          asm volatile("" :: "v"(bh[j & 1]), "v"(bl[j & 1]));
+          if (j == 0)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) asm volatile("" :: "v"(ah[i]), "v"(al[i]));
+        } else if constexpr (HI) {
 #pragma unroll
           for (int i = 0; i < TM; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
@@ -359,9 +370,10 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       // this wave's stores of step s done; barrier: every wave's too, and step s-1's reads of the
       // other slot are finished
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if constexpr ((MLIC_X4_ABL_RS & 4) == 0) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       auto staging = [&]() __attribute__((always_inline)) {
+        if constexpr ((MLIC_X4_ABL_RS & 1) != 0) return;
         if (s + 1 < s1) lstore(s + 1);
         if constexpr (HALO) {
           // the next chunk's halo: piece j - 1 stored and piece j loaded at local step j (the slot

@@ -275,5 +275,8 @@ int64_t chain_layer_halves(int Cout, int Cin);
 void chain_pack(const _Float16* wh, const _Float16* wl, int Cout, int Cin, int cin_pad, int permute, _Float16* dst,
                 hipStream_t st);
 void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st);
+// mlic_set_kernel_option("chain_nj"): 16-pixel column blocks per wave (-1 = $MLIC_CHAIN_NJ or 1; 2 = the
+// rounds 2-5 four-wave form); the same bits either way
+void chain_set_nj(int nj);
 
 }  // namespace mlic

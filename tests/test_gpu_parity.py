@@ -675,6 +675,29 @@ def test_entropy_parameters_chain_vs_oracle(kind, idx, cin):
     assert err <= 2e-5 * max(1.0, float(exp.abs().max())), PARITY[f"chain_ep_{kind}{idx}"]
 
 
+@pytest.mark.parametrize("kind,idx,cin", [("anchor", 0, 640), ("nonanchor", 9, 960)])
+def test_chain_wave_forms_same_bits(kind, idx, cin):
+    """The chain kernel's two wave layouts (mlic_set_kernel_option("chain_nj"): 1 = eight waves of 16
+    pixels, the default since round 6; 2 = four waves of 32 pixels) run every accumulator's MFMAs in the
+    same K order: the EntropyParameters outputs (ragged pixel tile) and a whole forward (LocalContext MLP
+    chains included) are bit-identical."""
+    net = net_for("MLICPP_L")
+    g = torch.Generator().manual_seed(7 + idx)
+    x = torch.randn(2, cin, 20, 28, generator=g) * 2
+    img = synthetic.synth_image(128, 192, 3).to(DEV)
+    outs = []
+    try:
+        for nj in (2, 1):
+            _lib.call("mlic_set_kernel_option", b"chain_nj", nj)
+            ep = net.run_module("epa" if kind == "anchor" else "epn", idx, x.to(DEV), out_shape=(2, 64, 20, 28)).cpu()
+            f = net(img)
+            outs.append((ep, f["x_hat"].cpu(), f["likelihoods"]["y_likelihoods"].cpu()))
+    finally:
+        _lib.call("mlic_set_kernel_option", b"chain_nj", -1)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("which,idx", [("inter", 3), ("inter", 9), ("intra", 1)])
 def test_linear_attention_fused_equals_unfused(golden, which, idx):
     """The fused linear attention (ctx = partials + the fixed-order combine, the output
