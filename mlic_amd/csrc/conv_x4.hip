@@ -22,6 +22,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace mlic {
 
@@ -77,6 +78,9 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 // per-step barrier -- wrong results, timing decomposition of the register-staged loop
 #ifndef MLIC_X4_ABL_RS
 #define MLIC_X4_ABL_RS 0
+#endif
+#ifndef MLIC_X4_STAGGER  // A/B build: 1 = staging point staggered between the two waves of a SIMD (measured
+#define MLIC_X4_STAGGER 0  // slower: g_s subpel conv 7.40 vs 7.08-7.13 ms, profiles/r06/ab/x4_stagger_halo_ab.log)
 #endif
 template <int K, int BM, bool RS, bool HI, bool DIR = false, bool HALO = false>
 __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float16* __restrict__ act,
@@ -290,7 +294,8 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     // hook: the step's staging work (next slot's LDS stores, the loads two steps ahead), issued after
     // the first pixel group's MFMAs, so that the step opens with its fragment reads and the LDS
     // latency they expose overlaps the staging's register waits instead of following them
-    auto mfma_step = [&](int s, auto&& hook) {
+    auto mfma_step = [&](int s, auto jh_c, auto&& hook) {
+      constexpr int JH = decltype(jh_c)::value;  // the pixel group after whose MFMAs the staging runs
       const char* As = sm + (s & 1) * A_BYTES;
       const char* Bs;
       int tapoff = 0;  // HALO: the tap's (ky, kx) shift in the halo image, in lines
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           for (int i = 0; i < TM; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
         }
-        if (j == 0) {
+        if (j == JH) {
           __builtin_amdgcn_sched_barrier(0);
           hook();
           __builtin_amdgcn_sched_barrier(0);
@@ -366,6 +371,12 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       lstore(s0);
     }
     if (s0 + 1 < s1) gload(s0 + 1);
+    // the K loop with the staging after pixel group JH.  STAGGER: the two waves of each SIMD (waves w and
+    // w + 4 of the workgroup share one) stage at different points of the step -- w < 4 after group 0,
+    // w >= 4 after group TN / 2 -- so that while one wave writes its LDS slot and waits for its loads, the
+    // other keeps the SIMD's matrix pipe busy (both at the same point left the pipe idle through the
+    // staging of both: timing decomposition, profiles/r06/ab/x4_ablation.log)
+    auto kloop = [&](auto jh_c) __attribute__((always_inline)) {
     for (int s = s0; s < s1; ++s) {
       // this wave's stores of step s done; barrier: every wave's too, and step s-1's reads of the
       // other slot are finished
@@ -389,10 +400,18 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       };
 #ifdef MLIC_X4_STAGING_FIRST  // A/B build: the round-3 order (staging, then the step's reads and MFMAs)
       staging();
-      mfma_step(s, [] {});
+      mfma_step(s, jh_c, [] {});
 #else
-      mfma_step(s, staging);
+      mfma_step(s, jh_c, staging);
 #endif
+    }
+    };
+    // (K x K convs only: the 1 x 1 direct form's two loop copies spill at the register cap)
+    if constexpr (MLIC_X4_STAGGER && K > 1) {
+      if (__builtin_amdgcn_readfirstlane(wave) & 4) kloop(std::integral_constant<int, TN / 2>{});
+      else kloop(std::integral_constant<int, 0>{});
+    } else {
+      kloop(std::integral_constant<int, 0>{});
     }
     if constexpr (DIR) range_report(P.rflag, f16_unsafe(__uint_as_float(dmax)));
   } else {
@@ -843,15 +862,18 @@ static bool x4_rs() {
 
 // the halo-staged B operand (conv_x4_kernel HALO) for a packed K x K stride-1 conv whose LDS images fit;
 // $MLIC_X4_HALO=0: B staged per tap (A/B switch)
-static int g_x4_halo = -1;  // mlic_set_kernel_option("x4_halo"): -1 = $MLIC_X4_HALO / default on
+static int g_x4_halo = -1;  // mlic_set_kernel_option("x4_halo"): -1 = $MLIC_X4_HALO / default (5 x 5 only)
 void x4_set_halo(int on) { g_x4_halo = on; }
-static bool x4_halo_on() {
-  static const bool env = [] {
+// 0 = off, 1 = 5 x 5 only (the default), 2 = 3 x 3 too ($MLIC_X4_HALO=2; the option's 1 means 3 x 3 too)
+static int x4_halo_setting() {
+  static const int env = [] {
     const char* e = std::getenv("MLIC_X4_HALO");
-    return !(e && std::atoi(e) == 0);
+    return e ? std::atoi(e) : 1;
   }();
-  return g_x4_halo < 0 ? env : g_x4_halo != 0;
+  if (g_x4_halo >= 0) return g_x4_halo == 0 ? 0 : 2;
+  return env;
 }
+static bool x4_halo_on() { return x4_halo_setting() != 0; }
 template <int K, int BM>
 constexpr bool x4_halo_fits() {
   constexpr int a = 2 * BM * ROWB, h = 2 * (TR + K - 1) * (TC + K - 1) * ROWB;
@@ -864,7 +886,7 @@ constexpr bool x4_halo_fits() {
 // 3x3 too (A/B), 0 turns it off.
 static bool x4_halo(const ConvParams& P, bool hi) {
   if (!x4_halo_on() || P.K == 1 || P.stride != 1) return false;
-  if (P.K == 3 && g_x4_halo != 1) return false;
+  if (P.K == 3 && x4_halo_setting() != 2) return false;
   const int bm = x4_bm(P.Cout);
   return 2 * bm * ROWB + 2 * (TR + P.K - 1) * (TC + P.K - 1) * ROWB <= 160 * 1024;
 }

@@ -71,7 +71,11 @@ inline void enc_put_bits(uint64_t& x, uint32_t*& ptr, uint32_t val, uint32_t nbi
 }
 }  // namespace
 
-RansEncoder::RansEncoder(int64_t n_hint) : out_((size_t)std::max<int64_t>(n_hint, 0) + 64, 0u) {
+// n_hint = the symbols to come; the first buffer holds n_hint / 16 words (2 bits per symbol; at the bench's
+// 0.1-0.5 bits per symbol a stream never grows, a high-rate one doubles a few times).  Round 6: it was one
+// word per symbol, zero-filled: 10.4 MB of memset and first-touch page faults per 1080p image, 41.8 MB per
+// 4K image, for a few hundred KB of stream
+RansEncoder::RansEncoder(int64_t n_hint) : out_((size_t)std::max<int64_t>(n_hint / 16, 0) + 1024, 0u) {
   end_ = out_.data() + out_.size();
   ptr_ = end_;
 }
@@ -167,6 +171,7 @@ bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S
   const int32_t* off = t.offset.data();
   const uint64_t* lut = t.lut.data();
   const int32_t* cdfs = t.cdf.data();
+  const CdfTables::Dom* dom = t.dom.data();
   const int stride = t.stride;
   const int32_t nhi = sizeof(S) < sizeof(int32_t) ? (int32_t)narrow_limit() : 0;  // the narrow range
   uint64_t state = state_;
@@ -174,18 +179,26 @@ bool RansDecoderState::decode(const I* indexes, int64_t n, const CdfTables& t, S
     const int32_t ci = (int32_t)indexes[i];
     if ((uint32_t)ci >= (uint32_t)t.n) throw std::runtime_error("rans: cdf index out of range");
     const uint32_t cum = (uint32_t)(state & mask);
-    const uint64_t e = lut[((size_t)ci << CdfTables::LUT_BITS) + (cum >> SHIFT)];
-    int32_t s = (int32_t)(e & 0xffff);
+    const CdfTables::Dom d = dom[ci];
+    int32_t s;
     uint32_t start, freq;
-    if (e >> 63) {
-      start = (uint32_t)(e >> 16) & 0xffff;
-      freq = (uint32_t)(e >> 32) & 0x1ffff;
+    if (cum - d.start < d.freq) {  // the dominant symbol (unsigned: cum below start wraps to a miss)
+      s = d.sym;
+      start = d.start;
+      freq = d.freq;
     } else {
-      const int32_t* cdf = cdfs + (int64_t)ci * stride;
-      const int32_t l = len[ci];
-      while (s < l - 1 && (uint32_t)cdf[s + 1] <= cum) ++s;
-      start = (uint32_t)cdf[s];
-      freq = (uint32_t)(cdf[s + 1] - cdf[s]);
+      const uint64_t e = lut[((size_t)ci << CdfTables::LUT_BITS) + (cum >> SHIFT)];
+      s = (int32_t)(e & 0xffff);
+      if (e >> 63) {
+        start = (uint32_t)(e >> 16) & 0xffff;
+        freq = (uint32_t)(e >> 32) & 0x1ffff;
+      } else {
+        const int32_t* cdf = cdfs + (int64_t)ci * stride;
+        const int32_t l = len[ci];
+        while (s < l - 1 && (uint32_t)cdf[s + 1] <= cum) ++s;
+        start = (uint32_t)cdf[s];
+        freq = (uint32_t)(cdf[s + 1] - cdf[s]);
+      }
     }
     const int32_t max_value = len[ci] - 2;
     if (s > max_value) throw std::runtime_error("rans: corrupt stream");
@@ -242,6 +255,7 @@ void CdfTables::prepare() {
   enc.assign((size_t)n * stride, EncSym{~0ull, 1, 0, 0, 0});
   const size_t L = (size_t)1 << LUT_BITS;
   lut.assign((size_t)n * L, 0);
+  dom.assign((size_t)n, Dom{0, 0, 0});
   for (int k = 0; k < n; ++k) {
     const int32_t* c = cdf.data() + (size_t)k * stride;
     const int len = length[k];
@@ -251,6 +265,14 @@ void CdfTables::prepare() {
       if (c[v + 1] <= c[v]) throw std::runtime_error("rans: cdf not strictly increasing");
       enc[(size_t)k * stride + v] = make_enc_sym((uint32_t)c[v], (uint32_t)(c[v + 1] - c[v]));
     }
+    // the dominant symbol among the regular ones (never the bypass escape len - 2)
+    int best = 0;
+    for (int v = 1; v < len - 2; ++v)
+      if (c[v + 1] - c[v] > c[best + 1] - c[best]) best = v;
+    // (only where it holds at least half the probability: a table whose dominant symbol is rarer would
+    // mostly miss, and a test that mostly misses costs a mispredicted branch; freq 0 = never taken)
+    const uint32_t bf = (uint32_t)(c[best + 1] - c[best]);
+    dom[(size_t)k] = Dom{(uint32_t)c[best], bf >= (1u << (PRECISION - 1)) ? bf : 0u, best};
     int s = 0;
     const uint32_t width = 1u << (PRECISION - LUT_BITS);
     for (size_t b = 0; b < L; ++b) {

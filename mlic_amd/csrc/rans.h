@@ -27,6 +27,15 @@ struct CdfTables {
   // [n][1 << LUT_BITS] decode buckets: bit 63 set => the whole bucket decodes to one symbol and the
   // entry holds (symbol | start << 16 | freq << 32); else the low 16 bits are the first candidate
   std::vector<uint64_t> lut;
+  // [n] the table's most probable symbol (largest frequency): its cdf start, its frequency and the symbol.
+  // The decoder tests the state's cum against this one range first -- a 12-byte record per table, L1-
+  // resident and independent of the state (loaded off the critical path) -- and only on a miss goes to the
+  // bucket table (512 KB: L2).  At the bench's rates the dominant symbol is most of the stream.
+  struct Dom {
+    uint32_t start, freq;
+    int32_t sym;
+  };
+  std::vector<Dom> dom;
   void prepare();
 };
 
