@@ -418,10 +418,16 @@ static int dw_mode(const ConvParams& P) {
 // (8 K pixels per image) the per-workgroup weight prologue outweighs the saved bytes (LRP: 4.14 vs
 // 4.3 ms unfused per 8 images, channel context slower), so the model fuses only grids of >= 16 K
 // pixels per image (dwpw_grid_ok)
+// Round 6: the Cin = Cout = 96 .. 192 forms are served by dwpw3_kernel (conv_dwpw3.hip) in the product;
+// their dwpw_kernel instantiations (the "dwpw2" option's form 0) are built into the A/B library only
+// (make AB=1 defines MLIC_AB_BUILD)
 #define DR_ALL(X, CIN, CT) X(CIN, CT, 0, 0) X(CIN, CT, 0, 1) X(CIN, CT, 1, 0) X(CIN, CT, 1, 1)
-#define DR_COMBOS(X)                                                                              \
-  DR_ALL(X, 192, 6) DR_ALL(X, 160, 5) DR_ALL(X, 128, 4) DR_ALL(X, 96, 3) DR_ALL(X, 48, 2)         \
-  X(224, 4, 1, 0) X(128, 1, 4, 1) X(192, 4, 1, 0)
+#if MLIC_AB_BUILD
+#define DR_EQ(X) DR_ALL(X, 192, 6) DR_ALL(X, 160, 5) DR_ALL(X, 128, 4) DR_ALL(X, 96, 3)
+#else
+#define DR_EQ(X)
+#endif
+#define DR_COMBOS(X) DR_EQ(X) DR_ALL(X, 48, 2) X(224, 4, 1, 0) X(128, 1, 4, 1) X(192, 4, 1, 0)
 
 bool dwpw_grid_ok(const ConvParams& P) { return (int64_t)P.H * P.W >= 16384; }
 
@@ -432,6 +438,7 @@ bool dwpw_ok(const ConvParams& P, int cin_pad) {
   if (P.Ho != P.H || P.Wo != P.W || P.out_cs != (int64_t)P.H * P.W || (P.W % 2) != 0) return false;
   const int64_t HW = (int64_t)P.H * P.W;
   if ((int64_t)P.Cin * HW * 4 >= (1ll << 31) || (int64_t)P.Cout * HW * 4 >= (1ll << 31)) return false;
+  if (dwpw2_ok(P, cin_pad)) return true;  // the Cin = Cout forms of the "dwpw2" option (dwpw3 by default)
   const int ct = (P.Cout + 31) / 32, res = (P.epi & EPI_RES) ? 1 : 0;
 #define DR_OK(CIN, CT, M, R) \
   if (P.Cin == CIN && ct == CT && mode == M && res == R) return true;
@@ -462,6 +469,7 @@ void dwpw_forward(const ConvParams& P, const _Float16* wh, const _Float16* wl, i
   }
   DR_COMBOS(DR_RUN)
 #undef DR_RUN
+  throw Error("mlic: dwpw_kernel for this shape is an A/B-only instantiation (the dwpw2 option's form 0: make AB=1)");
 }
 
 }  // namespace mlic

@@ -423,14 +423,15 @@ def test_dwpw_fused(B, Cn, H, W, epi):
     (1, 96, 33, 62, 1 | 64), (2, 160, 9, 130, 1), (1, 128, 70, 64, 1 | 64)])
 def test_dwpw2_fused(B, Cn, H, W, epi, form):
     """The fused Cin = Cout forms (mlic_set_kernel_option("dwpw2", form)): 0 = dwpw_kernel (conv_dwpw.hip,
-    one wave per SIMD), 1 = the row-pipelined LDS form (ab/conv_dwpw2.hip, A/B-only library), 2 = the
+    one wave per SIMD; its Cin = Cout instantiations are in the A/B library only since round 6), 1 = the
+    row-pipelined LDS form (ab/conv_dwpw2.hip, A/B-only library), 2 = the
     register-row form (conv_dwpw3.hip, the default; 64-pixel strips: ragged, narrower-than-a-strip and
     exact-multiple widths): the same bits as depthwise + resident pointwise.  (2, 192, 68, 120, GELU +
     residual) and (3, 192, 20, 96, residual) are the shapes on which form 1's masked-residual builds
     returned wrong rows."""
     from mlic_amd import _lib
-    if form == 1 and not _lib.ab_families():
-        pytest.skip("dwpw2 is an A/B-only kernel family (make AB=1)")
+    if form in (0, 1) and not _lib.ab_families():
+        pytest.skip("forms 0 / 1 are A/B-only instantiations for Cin = Cout (make AB=1)")
     _lib.call("mlic_set_kernel_option", b"dwpw2", form)
     try:
         _dwpw_case(B, Cn, Cn, H, W, epi)
