@@ -79,6 +79,9 @@ __device__ __forceinline__ half8 lds_frag(const char* base, int row, int granule
 #ifndef MLIC_X4_ABL_RS
 #define MLIC_X4_ABL_RS 0
 #endif
+#ifndef MLIC_X4_SPREAD  // A/B build: 1 = the staging loads/stores spread over the step's pixel groups, one slice
+#define MLIC_X4_SPREAD 0  // after each (measured slower: g_s subpel conv 7.79 vs 7.17 ms, main line 99.7 vs
+#endif                    // 103.4 img/s, profiles/r06/ab/x4_spread_staging_ab.log)
 #ifndef MLIC_X4_STAGGER  // A/B build: 1 = staging point staggered between the two waves of a SIMD (measured
 #define MLIC_X4_STAGGER 0  // slower: g_s subpel conv 7.40 vs 7.08-7.13 ms, profiles/r06/ab/x4_stagger_halo_ab.log)
 #endif
@@ -189,6 +192,7 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
     // A pieces (1 KB = 8 rows of the step's image) dealt round-robin over the 8 waves: piece
     // wave + 8 i (BM 96 has 12: waves 0-3 take two)
     constexpr int NPA = A_BYTES / 1024, NAR = (NPA + 7) / 8;
+    constexpr bool SPREAD = MLIC_X4_SPREAD && !DIR && !HALO && !HI;
     const _Float16* asrc_rs = wx + ((int64_t)ct * nsteps * BM) * ROWH + wave * 512 + lane * 8;
     u32x4 rb[(DIR || HALO) ? 1 : NB], ra[NAR];
     // HALO: pieces (16 bytes = one granule of one halo line) per thread per chunk; piece q of thread
@@ -290,6 +294,33 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
         if (NPA % 8 == 0 || wave + 8 * i < NPA)
           *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave + 8 * i) * 1024 + lane * 16) = ra[i];
     };
+    // SPREAD (plain register-staged form): the step's staging cut into its pieces (NB B pieces + NAR A
+    // pieces of 1 KB per wave), piece p stored and re-loaded after pixel group p * TN / NPC -- instead of
+    // all of them after group 0, where the 8 waves' 64 loads of a step met in the CU's address unit at
+    // one point (at 64 B/clk, ~1 k cycles during which every wave's in-order issue, MFMAs included,
+    // waited behind its loads: timing decomposition, profiles/r06/ab/x4_ablation.log)
+    constexpr int NPC = NB + NAR;
+    auto gload_piece = [&](int st, int p) __attribute__((always_inline)) {
+      if (p < NB) {
+        const int cc = st / KK, tap = st - cc * KK;
+        const int ky = tap / K, kx = tap - ky * K;
+        const int64_t d = cc * plane + ((int64_t)ky * Wp + kx) * ROWH;
+        rb[p] = *reinterpret_cast<const u32x4*>(bsrc[p] + d);
+      } else {
+        const int i = p - NB;
+        if (NPA % 8 == 0 || wave + 8 * i < NPA)
+          ra[i] = *reinterpret_cast<const u32x4*>(asrc_rs + (int64_t)st * BM * ROWH + i * 8 * 512);
+      }
+    };
+    auto lstore_piece = [&](int st, int p) __attribute__((always_inline)) {
+      if (p < NB) {
+        *reinterpret_cast<u32x4*>(sm + B_OFF + (st & 1) * B_BYTES + (wave * NB + p) * 1024 + lane * 16) = rb[p];
+      } else {
+        const int i = p - NB;
+        if (NPA % 8 == 0 || wave + 8 * i < NPA)
+          *reinterpret_cast<u32x4*>(sm + (st & 1) * A_BYTES + (wave + 8 * i) * 1024 + lane * 16) = ra[i];
+      }
+    };
     // step s's MFMAs on LDS slot s & 1 (fragment reads one pixel group ahead)
     // hook: the step's staging work (next slot's LDS stores, the loads two steps ahead), issued after
     // the first pixel group's MFMAs, so that the step opens with its fragment reads and the LDS
@@ -350,9 +381,16 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
           for (int i = 0; i < TM; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j & 1], acc[i][j], 0, 0, 0);
         }
-        if (j == JH) {
+        if constexpr (SPREAD) {
+          // this group's pieces (a compile-time range: j is unrolled)
+          if ((j + 1) * NPC / TN > j * NPC / TN) {
+            __builtin_amdgcn_sched_barrier(0);
+            hook(j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else if (j == JH) {
           __builtin_amdgcn_sched_barrier(0);
-          hook();
+          hook(j);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -383,8 +421,17 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if constexpr ((MLIC_X4_ABL_RS & 4) == 0) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      auto staging = [&]() __attribute__((always_inline)) {
+      auto staging = [&](int j) __attribute__((always_inline)) {
         if constexpr ((MLIC_X4_ABL_RS & 1) != 0) return;
+        if constexpr (SPREAD) {
+#pragma unroll
+          for (int p = 0; p < NPC; ++p)
+            if (p >= j * NPC / TN && p < (j + 1) * NPC / TN) {
+              if (s + 1 < s1) lstore_piece(s + 1, p);
+              if (s + 2 < s1) gload_piece(s + 2, p);
+            }
+          return;
+        }
         if (s + 1 < s1) lstore(s + 1);
         if constexpr (HALO) {
           // the next chunk's halo: piece j - 1 stored and piece j loaded at local step j (the slot
@@ -399,8 +446,8 @@ __global__ __launch_bounds__(X4T) void conv_x4_kernel(ConvParams P, const _Float
         if (s + 2 < s1) gload(s + 2);
       };
 #ifdef MLIC_X4_STAGING_FIRST  // A/B build: the round-3 order (staging, then the step's reads and MFMAs)
-      staging();
-      mfma_step(s, jh_c, [] {});
+      staging(0);
+      mfma_step(s, jh_c, [](int) {});
 #else
       mfma_step(s, jh_c, staging);
 #endif
