@@ -217,8 +217,36 @@ __global__ __launch_bounds__(LA_THREADS) void local_attn_mfma_kernel(LocalAttnPa
 // 5x5 "fusion" conv runs on conv_x4 with no fp32 round trip of the 800-row map and no packing pass.
 // Both heads are processed in one pass (two independent MFMA / softmax chains per pixel); loads
 // are branch-free (lanes outside the 25-cell window read a zero cell), q is pre-scaled at staging.
+#ifndef MLIC_LA_STAGE_V1  // A/B build: 1 = the element-per-thread staging of rounds 4-5
+#define MLIC_LA_STAGE_V1 0
+#endif
 namespace {
 constexpr int LP_TW = 32, LP_LW = LP_TW + 4, LP_NCELL = 5 * LP_LW, LP_NCP = LP_NCELL + 1;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t la_rsrc(const float* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+// key cell j of S^T accumulator register r in lane half h; its mask tables
+constexpr int la_j(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+constexpr uint32_t la_jbits(int h) {
+  uint32_t b = 0;
+  for (int r = 0; r < 16; ++r) b |= la_j(r, h) < 25 ? 1u << r : 0u;
+  return b;
+}
+constexpr uint32_t la_kbits(int h, int par) {  // key cells that are anchors at pixel parity par
+  uint32_t b = 0;
+  for (int r = 0; r < 16; ++r) {
+    const int j = la_j(r, h);
+    b |= (j < 25 && ((j / 5 + j % 5 + 1) & 1) == par) ? 1u << r : 0u;  // (par + jy + jx) odd
+  }
+  return b;
+}
+constexpr int la_voff(int t, int e, int h) {  // window-cell offset of key 16t + 8(e>>2) + 4h + (e&3), -1 past 25
+  const int j = 16 * t + 8 * (e >> 2) + 4 * h + (e & 3);
+  return j < 25 ? (j / 5) * LP_LW + j % 5 : -1;
+}
 }
 
 // Operands are split once at staging (not per use): q (pre-scaled) and k as [head][hi|lo][cell][16 d]
@@ -240,6 +268,7 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   const int ntx = (W + LP_TW - 1) / LP_TW;
   const int x0 = (blockIdx.x % ntx) * LP_TW, y0 = blockIdx.x / ntx;
   const float* src = P.qkv + (int64_t)b * P.qkv_bs;
+#if MLIC_LA_STAGE_V1
   // all of this thread's staging loads first (independent, in flight together), then the stores:
   // a load -> convert -> store loop serialises one full memory latency per element
   constexpr int NSTG = 3 * 32 * LP_NCP, NQ = (NSTG + LA_THREADS - 1) / LA_THREADS;
@@ -277,6 +306,54 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           (uint32_t)__builtin_bit_cast(uint16_t, hv) | ((uint32_t)__builtin_bit_cast(uint16_t, lv) << 16);
     }
   }
+#else
+  // thread t < 2 * LP_NCP stages window cell t % LP_NCP of the 48 channels of head t / LP_NCP
+  // (channel = d * heads + head, so channel c0 + 2q is tensor q >> 4, dim q & 15): one bounds test per
+  // thread, the 48 loads branch-free (an out-of-image cell reads 0 through an out-of-range buffer
+  // offset; the channel is the scalar offset) and in flight together, then q / k as two 16-byte hi and
+  // two lo rows and v as (hi, lo) words.  (Element per thread, the form before round 6: a bounds test,
+  // a branch and two 2-byte LDS stores per element -- 40 % of the kernel's VALU instructions.)
+  if (threadIdx.x < 2 * LP_NCP) {
+    const int c0 = threadIdx.x >= LP_NCP ? 1 : 0, cell = (int)threadIdx.x - c0 * LP_NCP;
+    const int gy = y0 - 2 + cell / LP_LW, gx = x0 - 2 + cell % LP_LW;
+    const bool in = cell < LP_NCELL && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const __amdgpu_buffer_rsrc_t rs = la_rsrc(src, (uint32_t)(96 * HW) * 4u);
+    const uint32_t vo = in ? (uint32_t)(c0 * HW + gy * W + gx) * 4u : 0x80000000u;
+    float v[48];
+#pragma unroll
+    for (int q = 0; q < 48; ++q)
+      v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (uint32_t)(2 * q * HW) * 4u, 0));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {  // q (pre-scaled), k
+      half8 hv[2], lv[2];
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        const float x = t == 0 ? v[d] * P.scale : v[16 + d];
+        const _Float16 hx = (_Float16)x;
+        hv[d >> 3][d & 7] = hx;
+        lv[d >> 3][d & 7] = (_Float16)(x - (float)hx);
+      }
+      _Float16* dst = sm + ((t * 2 + c0) * 2) * QKP + cell * 16;
+      *reinterpret_cast<half8*>(dst) = hv[0];
+      *reinterpret_cast<half8*>(dst + 8) = hv[1];
+      *reinterpret_cast<half8*>(dst + QKP) = lv[0];
+      *reinterpret_cast<half8*>(dst + QKP + 8) = lv[1];
+    }
+    uint32_t* vdst = reinterpret_cast<uint32_t*>(sm + QK_H) + c0 * 16 * LP_NCP + cell;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      const float x = v[32 + d];
+      const _Float16 hx = (_Float16)x, lx_ = (_Float16)(x - (float)hx);
+      vdst[d * LP_NCP] =
+          (uint32_t)__builtin_bit_cast(uint16_t, hx) | ((uint32_t)__builtin_bit_cast(uint16_t, lx_) << 16);
+    }
+  }
+  for (int i = threadIdx.x; i < 2 * 16 * 64; i += LA_THREADS) {
+    const int hh = i >> 10, r = (i >> 6) & 15, ln = i & 63, q32 = ln & 31;
+    const int j = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+    sbias[i] = (q32 < 25 && j < 25) ? P.rel_table[P.rel_index[q32 * 25 + j] * 2 + hh] : 0.0f;
+  }
+#endif
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -284,17 +361,10 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   const bool lvalid = l32 < 25;
   const int cy = lvalid ? l32 / 5 : 0, cx = lvalid ? l32 % 5 : 0;
   // interior mask bits for pixel parity 0 / 1: register r allowed iff query and key cell are anchors
-  uint32_t kbits[2] = {0u, 0u}, jbits = 0u;
+  // (compile-time tables per lane half h, selected once: no per-lane division by 5)
+  const uint32_t jbits = h ? la_jbits(1) : la_jbits(0);
+  const uint32_t kbits[2] = {h ? la_kbits(1, 0) : la_kbits(0, 0), h ? la_kbits(1, 1) : la_kbits(0, 1)};
   bool qok[2];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int jy = j / 5, jx = j - 5 * (j / 5);
-    if (j < 25) {
-      jbits |= 1u << r;
-      kbits[(jy + jx + 1) & 1] |= 1u << r;  // (par + jy + jx) odd
-    }
-  }
   qok[0] = lvalid && ((cy + cx) & 1);
   qok[1] = lvalid && !((cy + cx) & 1);
   // V^T gather: key j of element e of k-step t, as a window-cell offset (-1: outside the window or
@@ -303,10 +373,7 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int j = 16 * t + 8 * (e >> 2) + 4 * h + (e & 3);
-      voff[t][e] = (j < 25 && l32 < 16) ? (j / 5) * LP_LW + (j % 5) : -1;
-    }
+    for (int e = 0; e < 8; ++e) voff[t][e] = l32 < 16 ? (h ? la_voff(t, e, 1) : la_voff(t, e, 0)) : -1;
   const int vrow = l32 & 15;
 
   for (int lx = wave; lx < LP_TW; lx += LA_WAVES) {
@@ -325,11 +392,10 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       allow = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int j = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int jy = j / 5, jx = j - 5 * (j / 5);
+        const int jy = h ? la_j(r, 1) / 5 : la_j(r, 0) / 5, jx = h ? la_j(r, 1) % 5 : la_j(r, 0) % 5;
         const int kgy = py + jy - 2, kgx = px + jx - 2;
         const bool ka = kgy >= 0 && kgy < H && kgx >= 0 && kgx < W && ((par + jy + jx) & 1);
-        allow |= (qa && ka && j < 25) ? (1u << r) : 0u;
+        allow |= (qa && ka && ((jbits >> r) & 1u)) ? (1u << r) : 0u;
       }
     }
     _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + (int64_t)py * W + px) * 64;
