@@ -110,7 +110,10 @@ int mlic_set_poison(mlic_model* m, int on);
  * 544 x 960) on that kernel's pointwise form (-1 default = $MLIC_PW3 or 1: from 256 K px per image; 2: every
  * grid; 0 = pw_resident, the same bits); "narrow_limit" = L: coder symbols outside [-L - 1, L] cross PCIe
  * as int32 (the encoder's overflow copy, the decoder's int32 re-decode) -- a test knob for those fallback
- * paths, bitstreams unchanged (L <= 0: the int16 range, the default) */
+ * paths, bitstreams unchanged (L <= 0: the int16 range, the default); "chain_nj" = 16-pixel column blocks
+ * per wave of the fused 1x1 chain (-1 default = $MLIC_CHAIN_NJ or 1; 2 = four waves of 32 pixels, the same
+ * bits); "ep_half" = the slice loop's EntropyParameters chains over their own phase's checkerboard half
+ * (-1 default = $MLIC_EP_HALF or on; 0 = the whole grid: the same bits at every pixel that is read) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
  * tiles = conv impl 6, the VALU local attention = local-attention impl 0; `make AB=1`), else 0: the

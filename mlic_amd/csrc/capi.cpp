@@ -235,6 +235,7 @@ int mlic_set_kernel_option(const char* name, int value) {
     else if (n == "pw3") pw3_set(value);
     else if (n == "narrow_limit") set_narrow_limit(value);
     else if (n == "chain_nj") chain_set_nj(value);
+    else if (n == "ep_half") chain_set_ep_half(value);
     else throw Error("mlic: unknown kernel option " + n);
   });
 }

@@ -102,6 +102,17 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * CH_BN;
   const int HW = P.HW;
+  const int NQ = P.ckbd ? HW >> 1 : HW;  // pixels of this launch (the phase's half under ckbd)
+  // plane offset of the launch's pixel q (clamped: a ragged last tile loads the last pixel, stores nothing)
+  auto px_of = [&](int q) {
+    q = min(q, NQ - 1);
+    if (!P.ckbd) return q;
+    const int w2 = P.W >> 1, y = q / w2, x = 2 * (q - y * w2) + ((y + (P.ckbd == 1 ? 1 : 0)) & 1);
+    return y * P.W + x;
+  };
+  int pxj[NJ];  // the lane's pixels, one per 16-pixel column block
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) pxj[j] = px_of(p0 + PW * wv + 16 * j + l16);
   const int S0 = P.cin0 / 32;
   constexpr int S1 = C1 / 32, S2 = C2 / 32, S3 = C3 / 32;
   const int T = S0 + S1 + (NL > 2 ? S2 : 0) + (NL > 3 ? S3 : 0);
@@ -171,9 +182,8 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
     const float* src = P.seg[s].p + (int64_t)b * P.seg[s].bs + (int64_t)(ch - c0 + 8 * G) * HW;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int px = min(p0 + PW * wv + 16 * j + l16, HW - 1);  // ragged last tile: outputs dropped
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HW + px];
+      for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HW + pxj[j]];
     }
   };
 
@@ -215,7 +225,7 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
     const float* ax = P.aux + (int64_t)b * P.aux_bs;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int px = min(p0 + PW * wv + 16 * j + l16, HW - 1);
+      const int px = pxj[j];
 #pragma unroll
       for (int i = 0; i < C1 / 16; ++i)
 #pragma unroll
@@ -326,8 +336,8 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
     for (int i = 0; i < COUT / 16; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int px = p0 + PW * wv + 16 * j + l16;
-        if (px >= HW) continue;
+        if (p0 + PW * wv + 16 * j + l16 >= NQ) continue;
+        const int px = pxj[j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = 16 * i + 4 * G + e;
@@ -406,9 +416,22 @@ static int chain_nj() {
   return v == 2 ? 2 : 1;
 }
 
+// $MLIC_EP_HALF / mlic_set_kernel_option("ep_half"): EntropyParameters' chains run on their own
+// phase's checkerboard half only (ChainParams::ckbd); 0 = the whole grid (A/B, the same bits at every
+// pixel a consumer reads)
+static int g_ep_half = -1;
+void chain_set_ep_half(int on) { g_ep_half = on; }
+bool chain_ep_half() {
+  static const int env = [] {
+    const char* e = std::getenv("MLIC_EP_HALF");
+    return e ? std::atoi(e) : 1;
+  }();
+  return (g_ep_half >= 0 ? g_ep_half : env) != 0;
+}
+
 template <int NJ>
 static void launch_chain(const ChainParams& P, int nl, const int* cout, hipStream_t st) {
-  dim3 grid((P.HW + CH_BN - 1) / CH_BN, P.B);
+  dim3 grid(((P.ckbd ? P.HW / 2 : P.HW) + CH_BN - 1) / CH_BN, P.B);
   constexpr int T = ch_threads<NJ>();
   if (nl == 4 && cout[3] == 64)
     hipLaunchKernelGGL((chain_kernel<320, 256, 128, 64, NJ>), grid, dim3(T), 0, st, P);
@@ -423,6 +446,7 @@ void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st
   MLIC_CHECK(chain_supported(nl, cout), "chain: unsupported layer widths");
   MLIC_CHECK(P.cin0 % 64 == 0 && (P.cin0 > 0 || P.aux) && P.HW % 4 == 0 && P.HW >= 4,
              "chain: Cin multiple of 64 (or 0 with aux), HW of 4");
+  MLIC_CHECK(P.ckbd == 0 || (P.ckbd <= 2 && P.W > 0 && P.W % 2 == 0 && P.HW % P.W == 0), "chain: checkerboard half needs W even");
   if (chain_nj() == 2) launch_chain<2>(P, nl, cout, st);
   else launch_chain<1>(P, nl, cout, st);
 }

@@ -269,6 +269,11 @@ struct ChainParams {
   int* rflag;        // fp16 range guard (common.h range_check)
   const float* aux;  // optional [B][C1][HW] added to layer 0's pre-activation (hoisted part of layer 0)
   int64_t aux_bs;
+  // checkerboard half: 0 = every pixel; 1 = the anchor pixels only ((y + x) odd), 2 = the non-anchor
+  // pixels only (W even): the other half of every output plane is not written.  EntropyParameters'
+  // outputs are read at their own phase's pixels only (ckbd_anchor / ckbd_nonanchor masks,
+  // mlicpp.py:226-228, 239-241; quant_phase / phase_indexes / phase_dequant read `mine` pixels)
+  int ckbd, W;
 };
 bool chain_supported(int nl, const int* cout);
 int64_t chain_layer_halves(int Cout, int Cin);
@@ -278,5 +283,9 @@ void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st
 // mlic_set_kernel_option("chain_nj"): 16-pixel column blocks per wave (-1 = $MLIC_CHAIN_NJ or 1; 2 = the
 // rounds 2-5 four-wave form); the same bits either way
 void chain_set_nj(int nj);
+// mlic_set_kernel_option("ep_half"): EntropyParameters on its phase's half of the grid (-1 = $MLIC_EP_HALF
+// or on; 0 = the whole grid)
+void chain_set_ep_half(int on);
+bool chain_ep_half();
 
 }  // namespace mlic

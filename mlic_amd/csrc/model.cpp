@@ -697,7 +697,7 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
 
 // a fused chain over a (multi-segment) input; GELU between the layers (entropy.py:10-18, MLP fc1 -> fc2)
 void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
-                      const View* aux, int H, int W) {
+                      const View* aux, int H, int W, int ckbd) {
   ChainParams P{};
   MLIC_CHECK((int)ins.size() <= MAXSEG && (!ins.empty() || aux), "chain inputs");
   if (!ins.empty()) {
@@ -720,6 +720,8 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   }
   P.cin0 = cin;
   P.HW = H * W;
+  P.W = W;
+  P.ckbd = ckbd;
   P.B = L().B;
   for (int l = 0; l < 4; ++l) {
     P.bias[l] = c.bias[l];
@@ -736,7 +738,7 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   }
   double mac = (double)c.cin0 * c.cout[0];
   for (int l = 1; l < c.nl; ++l) mac += (double)c.cout[l - 1] * c.cout[l];
-  const double pix = (double)P.B * P.HW;
+  const double pix = (double)P.B * (ckbd ? P.HW / 2 : P.HW);
   const double bytes = 4.0 * (pix * (cin + out.C * (res ? 2 : 1) + (aux ? c.cout[0] : 0)) + mac);
   timed(PCAT_CHAIN, 2.0 * mac * pix, bytes, [&] { chain_forward(P, c.nl, c.cout, L().st); }, c.name);
 }
@@ -1116,24 +1118,27 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
 
 // entropy.py:7-29
 View Model::entropy_parameters(const std::vector<View>& ctx, const View* hyper, const std::string& kind, int i,
-                               const View* hoisted) {
+                               const View* hoisted, bool phase_only) {
   const std::string p = "entropy_parameters_" + kind + "." + std::to_string(i) + ".fusion";
   const View& geo = ctx.empty() ? *hyper : ctx[0];
   const int H = geo.H, W = geo.W;
+  // the phase's checkerboard half only: the reference computes the whole grid and masks the other half
+  // to zero (ckbd_anchor / ckbd_nonanchor, mlicpp.py:226-228, 239-241) before any use
+  const int ckbd = phase_only && chain_ep_half() && W % 2 == 0 ? (kind == "nonanchor" ? 2 : 1) : 0;
   const ConvW& l3 = cw(p + ".6");
   View out = alloc(l3.Cout, H, W);
   auto hc = chains_ctx_.find(p);
   if (hoisted && hc != chains_ctx_.end() && (H * W) % 4 == 0) {
     const int slot = 2 * i + (kind == "nonanchor" ? 1 : 0);
     const View aux = hoisted->ch(slot * hoist_rows_, hoist_rows_);
-    run_chain(hc->second, ctx, out, nullptr, &aux, H, W);
+    run_chain(hc->second, ctx, out, nullptr, &aux, H, W, ckbd);
     return out;
   }
   std::vector<View> ins = ctx;
   if (hyper) ins.push_back(*hyper);
   auto ch = chains_.find(p);
   if (chain_on() && ch != chains_.end() && (H * W) % 4 == 0) {
-    run_chain(ch->second, ins, out, nullptr);
+    run_chain(ch->second, ins, out, nullptr, nullptr, 0, 0, ckbd);
     return out;
   }
   const size_t m = L().arena.mark();
@@ -1246,12 +1251,12 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
     View ysl = yhat.ch(idx * C, C);
     View inter, chan, pa;
     if (idx == 0) {
-      pa = entropy_parameters({}, &hyper, "anchor", 0, hp);
+      pa = entropy_parameters({}, &hyper, "anchor", 0, hp, true);
     } else {
       View prev = yhat.ch(0, idx * C);
       inter = inter_context(prev, idx);
       chan = channel_context(prev, idx);
-      pa = entropy_parameters({inter, chan}, &hyper, "anchor", idx, hp);
+      pa = entropy_parameters({inter, chan}, &hyper, "anchor", idx, hp, true);
     }
     for (int ph = 0; ph < 2; ++ph) {
       QuantParams Q{};
@@ -1271,10 +1276,10 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       if (ph == 1) {
         View local = local_context(ysl, idx);
         if (idx == 0) {
-          pn = entropy_parameters({local}, &hyper, "nonanchor", 0, hp);
+          pn = entropy_parameters({local}, &hyper, "nonanchor", 0, hp, true);
         } else {
           View intra = intra_context(yhat.ch((idx - 1) * C, C), ysl, idx);
-          pn = entropy_parameters({local, intra, inter, chan}, &hyper, "nonanchor", idx, hp);
+          pn = entropy_parameters({local, intra, inter, chan}, &hyper, "nonanchor", idx, hp, true);
         }
       }
       const View& par = ph == 0 ? pa : pn;

@@ -261,7 +261,7 @@ class Model {
   void range_clear(Lane& l);
   int prec() const { return L().prec_force >= 0 ? L().prec_force : precision_; }
   void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
-                 const View* aux = nullptr, int H = 0, int W = 0);
+                 const View* aux = nullptr, int H = 0, int W = 0, int ckbd = 0);
   bool chain_on() const;
   bool dwpw_on() const;
   std::map<std::string, DwW> dws_;
@@ -332,9 +332,10 @@ class Model {
   View inter_context(const View& x, int i);
   View intra_context(const View& x1, const View& x2, int i);
   // ctx: the context segments of the layer-0 concat (entropy.py), hyper appended last; hoisted: the
-  // slice loop's precomputed W_hyp . hyper rows of all EPs (or null)
+  // slice loop's precomputed W_hyp . hyper rows of all EPs (or null); phase_only: the output is read at the
+  // kind's own checkerboard pixels only (the slice loop), so the chain may skip the other half
   View entropy_parameters(const std::vector<View>& ctx, const View* hyper, const std::string& kind, int i,
-                          const View* hoisted = nullptr);
+                          const View* hoisted = nullptr, bool phase_only = false);
   void lrp(const std::vector<View>& ins, const std::string& kind, int i, const View& yh_slice, bool anchor);
   View qkv_branch(const View& x, const std::string& p);
   void slice_loop(Mode mode, const View& hyper, const View* y, const View& yhat, float* y_lik, const CoderBufs* cb,

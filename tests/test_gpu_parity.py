@@ -698,6 +698,33 @@ def test_chain_wave_forms_same_bits(kind, idx, cin):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("hw", [(128, 192), (192, 320)])
+def test_ep_half_grid_same_bits(hw):
+    """Round 6: the slice loop's EntropyParameters chains run on their own phase's checkerboard half only
+    (mlic_set_kernel_option("ep_half"), on by default); the reference computes the whole grid and masks
+    the other half to zero before any use (mlicpp.py:226-228, 239-241).  forward() (x_hat, likelihoods),
+    compress() bytes and decompress() x_hat equal the whole-grid run's bit for bit -- with the workspace
+    NaN-poisoned (conftest), so a read of an unwritten pixel would show (latent widths 12 and 20: inputs
+    are multiples of 64, so a latent width is always even)."""
+    net = net_for("MLICPP_L")
+    net.update()
+    x = torch.cat([synthetic.synth_image(hw[0], hw[1], 80 + i) for i in range(2)]).to(DEV)
+    outs = []
+    try:
+        for half in (0, 1):
+            _lib.call("mlic_set_kernel_option", b"ep_half", half)
+            f = net(x)
+            c = net.compress(x)
+            d = net.decompress(c["strings"], c["shape"])
+            outs.append((f["x_hat"].cpu(), f["likelihoods"]["y_likelihoods"].cpu(), c["strings"], d["x_hat"].cpu()))
+    finally:
+        _lib.call("mlic_set_kernel_option", b"ep_half", -1)
+    (fx0, lk0, s0, dx0), (fx1, lk1, s1, dx1) = outs
+    assert s0 == s1
+    assert torch.equal(fx0, fx1) and torch.equal(lk0, lk1) and torch.equal(dx0, dx1)
+    assert torch.equal(dx1, fx1)
+
+
 @pytest.mark.parametrize("which,idx", [("inter", 3), ("inter", 9), ("intra", 1)])
 def test_linear_attention_fused_equals_unfused(golden, which, idx):
     """The fused linear attention (ctx = partials + the fixed-order combine, the output
