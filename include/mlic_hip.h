@@ -112,7 +112,8 @@ int mlic_set_poison(mlic_model* m, int on);
  * as int32 (the encoder's overflow copy, the decoder's int32 re-decode) -- a test knob for those fallback
  * paths, bitstreams unchanged (L <= 0: the int16 range, the default); "chain_nj" = 16-pixel column blocks
  * per wave of the fused 1x1 chain (-1 default = $MLIC_CHAIN_NJ or 1; 2 = four waves of 32 pixels, the same
- * bits); "ep_half" = the slice loop's EntropyParameters chains over their own phase's checkerboard half
+ * bits); "ep_half" = the slice loop's EntropyParameters chains (and its LocalContext, read by the non-anchor
+ * EntropyParameters only) over their own phase's checkerboard half
  * (-1 default = $MLIC_EP_HALF or on; 0 = the whole grid: the same bits at every pixel that is read) */
 int mlic_set_kernel_option(const char* name, int value);
 /* 1 when this library holds the A/B-only kernel families (v1 split-fp16 tiles = precision 1, the halo
@@ -171,6 +172,11 @@ int mlic_local_attn_run(void* stream, int impl, const float* qkv, const float* r
    [B][25][npos][64], npos = ceil(H*W / 32) * 32; channel k = head*16 + d, hi at k, lo at 32 + k */
 int mlic_local_attn_packed_run(void* stream, const float* qkv, const float* rel_table, const int32_t* rel_index,
                                uint16_t* out, int H, int W, int B, float scale);
+/* the same for one checkerboard phase's query pixels only (ckbd 1: anchors, (y + x) odd; 2: non-anchors;
+   W even), written at the squeezed position y * W / 2 + x / 2: npos = ceil(H*W/2 / 32) * 32 (round 6: the
+   slice loop's LocalContext, whose only consumer reads the non-anchor pixels) */
+int mlic_local_attn_packed_half_run(void* stream, const float* qkv, const float* rel_table, const int32_t* rel_index,
+                                    uint16_t* out, int H, int W, int B, float scale, int ckbd);
 int mlic_image_sq_err_u8(void* stream, const float* a, const float* b, int B, int64_t n_per, double* out);
 /* per-image sum of -log2(lik) over n_per elements (fixed reduction order); synchronous */
 int mlic_neglog2_sum(void* stream, const float* lik, int B, int64_t n_per, double* out);

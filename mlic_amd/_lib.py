@@ -63,6 +63,7 @@ def _sig(lib):
         "mlic_dwpw_run": [p, p, p, p, p, p, p, i, i, i, i, i, i, p],
         "mlic_local_attn_run": [p, i, p, p, p, p, i, i, i, i, f],
         "mlic_local_attn_packed_run": [p, p, p, p, p, i, i, i, f],
+        "mlic_local_attn_packed_half_run": [p, p, p, p, p, i, i, i, f, i],
         "mlic_image_sq_err_u8": [p, p, p, i, i64, p],
         "mlic_neglog2_sum": [p, p, i, i64, p],
         "mlic_gaussian_likelihood": [p, p, p, p, i64, f, p],

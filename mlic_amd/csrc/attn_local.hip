@@ -376,7 +376,11 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     for (int e = 0; e < 8; ++e) voff[t][e] = l32 < 16 ? (h ? la_voff(t, e, 1) : la_voff(t, e, 0)) : -1;
   const int vrow = l32 & 15;
 
-  for (int lx = wave; lx < LP_TW; lx += LA_WAVES) {
+  // ckbd: this row's pixels of one checkerboard phase only (x0 is even, so a fixed column parity)
+  const int xoff = P.ckbd ? ((y0 + (P.ckbd == 1 ? 1 : 0)) & 1) : 0;
+  const int nlx = P.ckbd ? LP_TW / 2 : LP_TW;
+  for (int k = wave; k < nlx; k += LA_WAVES) {
+    const int lx = P.ckbd ? 2 * k + xoff : k;
     const int px = x0 + lx, py = y0;
     if (px >= W) break;  // wave-uniform
     const int qcell = lvalid ? cy * LP_LW + lx + cx : LP_NCELL;
@@ -398,7 +402,8 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         allow |= (qa && ka && ((jbits >> r) & 1u)) ? (1u << r) : 0u;
       }
     }
-    _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + (int64_t)py * W + px) * 64;
+    const int64_t pos = P.ckbd ? ((int64_t)py * W + px) >> 1 : (int64_t)py * W + px;
+    _Float16* dst = outp + (((int64_t)b * 25 + l32) * npos + pos) * 64;
     // one head at a time, start to store: only one S and one O accumulator live (<= 128 VGPRs, so
     // two workgroups share a CU and one's staging overlaps the other's products)
 #pragma unroll
@@ -472,7 +477,8 @@ __global__ __launch_bounds__(LA_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 
 void local_attn_packed(const LocalAttnParams& P, _Float16* out, int npos, hipStream_t st) {
   MLIC_CHECK(P.C == 32, "packed LocalContext attention: dim 32 (2 heads x 16)");
-  MLIC_CHECK(npos >= P.H * P.W, "packed output positions");
+  MLIC_CHECK(P.ckbd == 0 || (P.ckbd <= 2 && P.W % 2 == 0), "packed attention: checkerboard half needs W even");
+  MLIC_CHECK(npos >= (P.ckbd ? P.H * P.W / 2 : P.H * P.W), "packed output positions");
   const int ntx = (P.W + LP_TW - 1) / LP_TW;
   hipLaunchKernelGGL(local_attn_packed_kernel, dim3(ntx * P.H, P.B), dim3(LA_THREADS), 0, st, P, out, npos);
   HIP_OK(hipGetLastError());

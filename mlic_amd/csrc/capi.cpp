@@ -569,6 +569,23 @@ int mlic_local_attn_packed_run(void* stream, const float* qkv, const float* rel_
   });
 }
 
+int mlic_local_attn_packed_half_run(void* stream, const float* qkv, const float* rel_table, const int32_t* rel_index,
+                                    uint16_t* out, int H, int W, int B, float scale, int ckbd) {
+  return guard([&] {
+    MLIC_CHECK(ckbd == 1 || ckbd == 2, "ckbd: 1 (anchors) or 2 (non-anchors)");
+    LocalAttnParams A{};
+    A.qkv = qkv;
+    A.qkv_bs = (int64_t)3 * 32 * H * W;
+    A.rel_table = rel_table;
+    A.rel_index = rel_index;
+    A.scale = scale;
+    A.C = 32; A.H = H; A.W = W; A.B = B;
+    A.ckbd = ckbd;
+    local_attn_packed(A, reinterpret_cast<_Float16*>(out), (H * W / 2 + 31) / 32 * 32, (hipStream_t)stream);
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  });
+}
+
 int mlic_local_attn_mask(void* stream, float* out, int H, int W) {
   return guard([&] { local_mask(out, H, W, (hipStream_t)stream); });
 }

@@ -110,9 +110,16 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
     const int w2 = P.W >> 1, y = q / w2, x = 2 * (q - y * w2) + ((y + (P.ckbd == 1 ? 1 : 0)) & 1);
     return y * P.W + x;
   };
-  int pxj[NJ];  // the lane's pixels, one per 16-pixel column block
+  // the lane's pixels, one per 16-pixel column block: in the input / residual / aux planes (squeezed
+  // planes of NQ pixels under sq_in) and in the output planes
+  const int HWi = P.sq_in ? NQ : HW;
+  int pxj[NJ], pxo[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) pxj[j] = px_of(p0 + PW * wv + 16 * j + l16);
+  for (int j = 0; j < NJ; ++j) {
+    const int q = p0 + PW * wv + 16 * j + l16;
+    pxo[j] = px_of(q);
+    pxj[j] = P.sq_in ? min(q, NQ - 1) : pxo[j];
+  }
   const int S0 = P.cin0 / 32;
   constexpr int S1 = C1 / 32, S2 = C2 / 32, S3 = C3 / 32;
   const int T = S0 + S1 + (NL > 2 ? S2 : 0) + (NL > 3 ? S3 : 0);
@@ -179,11 +186,11 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
     const int ch = 32 * t;
     int s = 0, c0 = 0;
     while (s + 1 < P.nseg && ch >= c0 + P.seg[s].C) { c0 += P.seg[s].C; ++s; }
-    const float* src = P.seg[s].p + (int64_t)b * P.seg[s].bs + (int64_t)(ch - c0 + 8 * G) * HW;
+    const float* src = P.seg[s].p + (int64_t)b * P.seg[s].bs + (int64_t)(ch - c0 + 8 * G) * HWi;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HW + pxj[j]];
+      for (int kk = 0; kk < 8; ++kk) f[j][kk] = src[(int64_t)kk * HWi + pxj[j]];
     }
   };
 
@@ -229,7 +236,7 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
 #pragma unroll
       for (int i = 0; i < C1 / 16; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc0[i][j][e] = ldexpf(ax[(int64_t)(16 * i + 4 * G + e) * HW + px], P.wexp[0]);
+        for (int e = 0; e < 4; ++e) acc0[i][j][e] = ldexpf(ax[(int64_t)(16 * i + 4 * G + e) * HWi + px], P.wexp[0]);
     }
   } else {
 #pragma unroll
@@ -337,13 +344,13 @@ __global__ __launch_bounds__(ch_threads<NJ>()) void chain_kernel(ChainParams P) 
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (p0 + PW * wv + 16 * j + l16 >= NQ) continue;
-        const int px = pxj[j];
+        const int px = pxo[j], pxi = pxj[j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = 16 * i + 4 * G + e;
           float v = __builtin_fmaf(acc[i][j][e], unscale, sbias[boff + co]);
           bad |= !(__builtin_fabsf(v) <= 3.4e38f) ? 1 : 0;
-          if (P.res) v += P.res[(int64_t)b * P.res_bs + (int64_t)co * HW + px];
+          if (P.res) v += P.res[(int64_t)b * P.res_bs + (int64_t)co * HWi + pxi];
           P.out[(int64_t)b * P.out_bs + (int64_t)co * HW + px] = v;
         }
       }
@@ -447,6 +454,7 @@ void chain_forward(const ChainParams& P, int nl, const int* cout, hipStream_t st
   MLIC_CHECK(P.cin0 % 64 == 0 && (P.cin0 > 0 || P.aux) && P.HW % 4 == 0 && P.HW >= 4,
              "chain: Cin multiple of 64 (or 0 with aux), HW of 4");
   MLIC_CHECK(P.ckbd == 0 || (P.ckbd <= 2 && P.W > 0 && P.W % 2 == 0 && P.HW % P.W == 0), "chain: checkerboard half needs W even");
+  MLIC_CHECK(!P.sq_in || P.ckbd, "chain: squeezed inputs need a checkerboard half");
   if (chain_nj() == 2) launch_chain<2>(P, nl, cout, st);
   else launch_chain<1>(P, nl, cout, st);
 }

@@ -160,6 +160,9 @@ struct LocalAttnParams {
   const int* rel_index;    // [625] int32
   float scale;
   int C, H, W, B;
+  // local_attn_packed only: 0 = every query pixel; 1 / 2 = the anchor / non-anchor pixels only, written
+  // at their squeezed position y * W / 2 + x / 2 (W even)
+  int ckbd;
 };
 void local_attn(const LocalAttnParams& P, hipStream_t st);       // MFMA (attn_local.hip) unless MLIC_LOCAL_ATTN_VALU=1
 void local_attn_mfma(const LocalAttnParams& P, hipStream_t st);
@@ -274,6 +277,7 @@ struct ChainParams {
   // outputs are read at their own phase's pixels only (ckbd_anchor / ckbd_nonanchor masks,
   // mlicpp.py:226-228, 239-241; quant_phase / phase_indexes / phase_dequant read `mine` pixels)
   int ckbd, W;
+  int sq_in;  // with ckbd: the inputs and the residual are squeezed planes of HW / 2 pixels (pixel q at q)
 };
 bool chain_supported(int nl, const int* cout);
 int64_t chain_layer_halves(int Cout, int Cin);

@@ -697,7 +697,7 @@ void Model::dw(const std::vector<View>& ins, const DwW& w, int stride, const Vie
 
 // a fused chain over a (multi-segment) input; GELU between the layers (entropy.py:10-18, MLP fc1 -> fc2)
 void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
-                      const View* aux, int H, int W, int ckbd) {
+                      const View* aux, int H, int W, int ckbd, bool sq_in) {
   ChainParams P{};
   MLIC_CHECK((int)ins.size() <= MAXSEG && (!ins.empty() || aux), "chain inputs");
   if (!ins.empty()) {
@@ -712,6 +712,8 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
     cin += ins[s].C;
   }
   MLIC_CHECK(cin == c.cin0, "chain Cin mismatch");
+  MLIC_CHECK(!sq_in || (ckbd && !aux), "chain: squeezed inputs need a checkerboard half");
+  if (sq_in) W *= 2;  // squeezed input planes (H x W / 2): the output is the full grid
   MLIC_CHECK(out.C == c.cout[c.nl - 1] && out.H == H && out.W == W, "chain output shape");
   if (aux) {
     MLIC_CHECK(aux->C == c.cout[0] && aux->H == H && aux->W == W, "chain aux shape");
@@ -722,6 +724,7 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   P.HW = H * W;
   P.W = W;
   P.ckbd = ckbd;
+  P.sq_in = sq_in ? 1 : 0;
   P.B = L().B;
   for (int l = 0; l < 4; ++l) {
     P.bias[l] = c.bias[l];
@@ -732,7 +735,7 @@ void Model::run_chain(const ChainW& c, const std::vector<View>& ins, const View&
   P.out = out.p;
   P.out_bs = out.bs;
   if (res) {
-    MLIC_CHECK(res->C == out.C && res->H == out.H && res->W == out.W, "chain residual shape");
+    MLIC_CHECK(res->C == out.C && res->H == out.H && res->W * (sq_in ? 2 : 1) == out.W, "chain residual shape");
     P.res = res->p;
     P.res_bs = res->bs;
   }
@@ -918,26 +921,34 @@ void Model::g_s(const View& yh, const View& out) {
 
 // ------------------------------------------------------------------------------------- MEM++
 // context.py:67-112 LocalContext
-View Model::local_context(const View& x, int i) {
+View Model::local_context(const View& x, int i, bool half) {
   const std::string p = "local_context." + std::to_string(i);
   const int C = x.C, H = x.H, W = x.W;
   View out = alloc(2 * C, H, W);
   const size_t m = L().arena.mark();
+  static const bool packed_on = [] {  // $MLIC_LA_PACKED=0: the unfolded fp32 path (A/B switch)
+    const char* e = std::getenv("MLIC_LA_PACKED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const bool packed = packed_on && prec() == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm");
+  // non-anchor half only: every stage after the qkv projection is per query pixel, so it runs on the
+  // squeezed half (planes of H x W / 2, pixel y W / 2 + x / 2) and the MLP chain writes the full-grid
+  // output at the non-anchor pixels (the reference computes the whole grid; its only consumer, the
+  // non-anchor EntropyParameters, reads these pixels: mlicpp.py:237-241, 267-271)
+  auto cit = chains_.find(p + ".mlp");
+  half = half && packed && W % 2 == 0 && chain_on() && cit != chains_.end() && (H * W) % 8 == 0;
+  const int Wq = half ? W / 2 : W;
   View n1 = alloc(C, H, W);
   const double pix = (double)L().B * H * W;
   timed(PCAT_ELEM, 8.0 * pix * C, 8.0 * pix * C, [&] {
     ln_channels(x.p, x.bs, n1.p, n1.bs, rw(p + ".norm1.weight"), rw(p + ".norm1.bias"), C, H * W, L().B, L().st);
   }, p + ".norm1");
   View qkv = conv1x1(n1, p + ".qkv_proj", 1, EPI_NONE);
-  View f = alloc(2 * C, H, W);
-  static const bool packed_on = [] {  // $MLIC_LA_PACKED=0: the unfolded fp32 path (A/B switch)
-    const char* e = std::getenv("MLIC_LA_PACKED");
-    return !(e && std::atoi(e) == 0);
-  }();
-  if (packed_on && prec() == PREC_F16X3_V2 && C == 32 && convs_.count(p + ".fusion.__x4perm")) {
+  View f = alloc(2 * C, H, Wq);
+  if (packed) {
     // attention straight into the fusion conv's packed split operand, fusion on conv_x4
     const ConvW& fw = cw(p + ".fusion.__x4perm");
-    const int npos = (H * W + 31) / 32 * 32;
+    const int npos = (H * Wq + 31) / 32 * 32;
     _Float16* tp = reinterpret_cast<_Float16*>(L().arena.alloc((int64_t)L().B * 25 * npos * 32));
     LocalAttnParams A{};
     A.qkv = qkv.p;
@@ -949,9 +960,11 @@ View Model::local_context(const View& x, int i) {
     A.H = H;
     A.W = W;
     A.B = L().B;
-    const double fl = pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
-    timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + 25 * C), [&] { local_attn_packed(A, tp, npos, L().st); }, p + ".attn");
-    const View tv{nullptr, 25 * C, H, W, (int64_t)25 * C * H * W};  // geometry only: conv_x4 reads tp
+    A.ckbd = half ? 2 : 0;
+    const double fl = (half ? 0.5 : 1.0) * pix * 2.0 * 2 * 25 * 25 * (C / 2) * 2;
+    timed(PCAT_LOCAL, fl, 4.0 * pix * (3 * C + (half ? 0.5 : 1.0) * 25 * C), [&] { local_attn_packed(A, tp, npos, L().st); },
+          p + ".attn");
+    const View tv{nullptr, 25 * C, H, Wq, (int64_t)25 * C * H * Wq};  // geometry only: conv_x4 reads tp
     run_conv(conv_params({tv}, fw, 1, 0, f, EPI_NONE, nullptr, nullptr), fw, tp);
   } else {
   View t = alloc(25 * C, H, W);
@@ -975,12 +988,15 @@ View Model::local_context(const View& x, int i) {
   conv({t}, cw(p + ".fusion"), 1, 0, f, EPI_NONE);
   }
   View pj = conv1x1(f, p + ".proj", 1, EPI_NONE);
-  View n2 = alloc(2 * C, H, W);
-  timed(PCAT_ELEM, 16.0 * pix * C, 16.0 * pix * C, [&] {
-    ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * W, L().B, L().st);
+  View n2 = alloc(2 * C, H, Wq);
+  const double pq = (double)L().B * H * Wq;
+  timed(PCAT_ELEM, 16.0 * pq * C, 16.0 * pq * C, [&] {
+    ln_channels(pj.p, pj.bs, n2.p, n2.bs, rw(p + ".norm2.weight"), rw(p + ".norm2.bias"), 2 * C, H * Wq, L().B, L().st);
   }, p + ".norm2");
-  auto ch = chains_.find(p + ".mlp");
-  if (chain_on() && ch != chains_.end() && (H * W) % 4 == 0) {
+  auto ch = cit;
+  if (half) {
+    run_chain(ch->second, {n2}, out, &pj, nullptr, 0, 0, 2, true);
+  } else if (chain_on() && ch != chains_.end() && (H * W) % 4 == 0) {
     run_chain(ch->second, {n2}, out, &pj);
   } else {
     View h1 = conv1x1(n2, p + ".mlp.fc1", 1, EPI_GELU);
@@ -1117,6 +1133,12 @@ View Model::intra_context(const View& x1, const View& x2, int i) {
 }
 
 // entropy.py:7-29
+bool Model::ep_half_chain(const std::string& kind, int i, int H, int W, bool hoisted) const {
+  const std::string p = "entropy_parameters_" + kind + "." + std::to_string(i) + ".fusion";
+  if (!chain_ep_half() || W % 2 != 0 || (H * W) % 4 != 0) return false;
+  return hoisted ? chains_ctx_.count(p) > 0 : (chain_on() && chains_.count(p) > 0);
+}
+
 View Model::entropy_parameters(const std::vector<View>& ctx, const View* hyper, const std::string& kind, int i,
                                const View* hoisted, bool phase_only) {
   const std::string p = "entropy_parameters_" + kind + "." + std::to_string(i) + ".fusion";
@@ -1274,7 +1296,7 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
       Q.phase = ph;
       View pn;
       if (ph == 1) {
-        View local = local_context(ysl, idx);
+        View local = local_context(ysl, idx, ep_half_chain("nonanchor", idx, H, W, hp != nullptr));
         if (idx == 0) {
           pn = entropy_parameters({local}, &hyper, "nonanchor", 0, hp, true);
         } else {

@@ -261,7 +261,7 @@ class Model {
   void range_clear(Lane& l);
   int prec() const { return L().prec_force >= 0 ? L().prec_force : precision_; }
   void run_chain(const ChainW& c, const std::vector<View>& ins, const View& out, const View* res,
-                 const View* aux = nullptr, int H = 0, int W = 0, int ckbd = 0);
+                 const View* aux = nullptr, int H = 0, int W = 0, int ckbd = 0, bool sq_in = false);
   bool chain_on() const;
   bool dwpw_on() const;
   std::map<std::string, DwW> dws_;
@@ -327,7 +327,11 @@ class Model {
   View h_a(const View& y);
   View h_s(const View& z_hat);
   void g_s(const View& y_hat, const View& out);
-  View local_context(const View& x, int i);
+  // half: the output is read at the non-anchor pixels only (the slice loop, when the non-anchor
+  // EntropyParameters runs on its half: ep_half_chain) -- attention, fusion, norm and MLP on that half
+  View local_context(const View& x, int i, bool half = false);
+  // the slice loop's EntropyParameters of (kind, i) will run as a chain over its phase's half of the grid
+  bool ep_half_chain(const std::string& kind, int i, int H, int W, bool hoisted) const;
   View channel_context(const View& x, int i);
   View inter_context(const View& x, int i);
   View intra_context(const View& x1, const View& x2, int i);

@@ -632,6 +632,33 @@ def test_local_attention_packed(H, W, B):
     assert d.max().item() <= 1e-3 * expect.abs().max().item(), d.max().item()
 
 
+@pytest.mark.parametrize("H,W,B", [(24, 40, 2), (68, 120, 1), (14, 22, 1)])
+def test_local_attention_packed_half(H, W, B):
+    """Round 6: the packed attention over one checkerboard phase's query pixels (the slice loop's
+    LocalContext runs it on the non-anchor half): bit-identical to the whole-grid kernel's output at those
+    pixels, written at their squeezed positions y * W / 2 + x / 2."""
+    from mlic_amd import _lib, synthetic
+    g = torch.Generator().manual_seed(6)
+    dev = torch.device("cuda")
+    qkv = (torch.randn(B, 96, H, W, generator=g) * 2).to(dev)
+    table = torch.randn(81, 2, generator=g).to(dev)
+    index = torch.from_numpy(synthetic.relative_position_index(5)).reshape(-1).to(torch.int32).to(dev)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    npos = (H * W + 31) // 32 * 32
+    full = torch.zeros(B, 25, npos, 64, dtype=torch.int16, device=dev)
+    _lib.call("mlic_local_attn_packed_run", st, C.c_void_p(qkv.data_ptr()), C.c_void_p(table.data_ptr()),
+              C.c_void_p(index.data_ptr()), C.c_void_p(full.data_ptr()), H, W, B, 0.25)
+    yy, xx = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    for ckbd in (1, 2):
+        nq = (H * W // 2 + 31) // 32 * 32
+        half = torch.zeros(B, 25, nq, 64, dtype=torch.int16, device=dev)
+        _lib.call("mlic_local_attn_packed_half_run", st, C.c_void_p(qkv.data_ptr()), C.c_void_p(table.data_ptr()),
+                  C.c_void_p(index.data_ptr()), C.c_void_p(half.data_ptr()), H, W, B, 0.25, ckbd)
+        sel = (((yy + xx) % 2) == (1 if ckbd == 1 else 0)).reshape(-1)   # anchors: (y + x) odd
+        want = full[:, :, :H * W][:, :, sel.to(dev)]
+        assert torch.equal(half[:, :, :H * W // 2], want), ckbd
+
+
 # split-fp16 operand range (conv_f16x3.hip header): tiny weights (the per-row power-of-two prescale keeps
 # their lo halves normal) and activations up to 1e3, every split family, against float64
 @pytest.mark.parametrize("impl,Cin,Cout,H,W,K", [(X3V2, 192, 320, 24, 40, 1), (X3V2, 96, 96, 20, 36, 3),
