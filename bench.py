@@ -124,7 +124,7 @@ def parse(argv=None):
     ap.add_argument("--split", type=int, default=0,
                     help="cut each (weights, shape) batch into this many request streams, each an independent "
                          "compress -> decompress chain on its own model instance (0: the workload's default)")
-    ap.add_argument("--schedule", choices=["join", "streams"], default="join",
+    ap.add_argument("--schedule", choices=["join", "streams"], default=os.environ.get("MLIC_SCHEDULE", "streams"),
                     help="join: the batches of a step meet at a join every step; streams: when every batch has "
                          "its own worker, each runs its K steps back to back")
     ap.add_argument("--emulate-world", type=int, default=0,
@@ -394,6 +394,12 @@ def main(argv=None):
             n = n.to(dev).eval()
             n.update()
             n.set_lanes(a.lanes)
+            if conc > 1 and os.environ.get("MLIC_GROUP_PRIO", "0") != "0":
+                # A/B (MLIC_GROUP_PRIO=1): staggered stream priorities across the concurrent groups' models
+                # (group g's lanes after group g - 1's).  Measured slower (main line 103.8-105.7 vs
+                # 105.4-106.5 img/s, profiles/r06/ab/group_priority_ab.log): with 3 priority levels the
+                # low-priority groups are starved into a serial tail at the end of every step
+                n.set_priority_base(gi * a.lanes)
             n.set_precision(a.precision)
             n.set_synthesis_precision(1 if a.synth_fp16 else 0)
             nets[key] = n

@@ -54,6 +54,11 @@ int mlic_set_entropy_tables(mlic_model* m, const int32_t* gc_cdf, const int32_t*
  * workspace, so the host rANS coding of one lane overlaps the kernels of another (default 4, or
  * $MLIC_LANES).  Results are identical for any lane count. */
 int mlic_set_lanes(mlic_model* m, int lanes);
+/* the lanes' HIP stream priorities are staggered (lane 0 highest, $MLIC_LANE_PRIORITY=0 disables); `base`
+ * offsets this model's lanes (lane i at greatest + base + i, clamped to the device's range), so request
+ * streams served by separate models drift apart as well.  Applies to lanes created afterwards (a model
+ * creates its lanes on first use).  Scheduling only: results do not depend on it. */
+int mlic_set_priority_base(mlic_model* m, int base);
 int mlic_compress(mlic_model* m, void* stream, const float* x, int B, int H, int W, float vbr_scale);
 int mlic_compress_v(mlic_model* m, void* stream, const float* x, int B, int H, int W, const float* vbr_scales);
 int mlic_encoded_size(mlic_model* m, int b, size_t* y_len, size_t* z_len);

@@ -43,6 +43,7 @@ def _sig(lib):
         "mlic_local_attn_mask": [p, p, i, i],
         "mlic_set_profiling": [p, i],
         "mlic_set_lanes": [p, i],
+        "mlic_set_priority_base": [p, i],
         "mlic_set_precision": [p, i],
         "mlic_set_synthesis_precision": [p, i],
         "mlic_set_poison": [p, i],

@@ -270,6 +270,13 @@ int mlic_set_lanes(mlic_model* m, int lanes) {
   return guard([&] { impl(m).set_lanes(lanes); });
 }
 
+int mlic_set_priority_base(mlic_model* m, int base) {
+  return guard([&] {
+    MLIC_CHECK(base >= 0, "priority base must be >= 0");
+    impl(m).set_priority_base(base);
+  });
+}
+
 int mlic_set_profiling(mlic_model* m, int on) {
   return guard([&] { impl(m).set_profiling(on != 0); });
 }

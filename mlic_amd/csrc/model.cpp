@@ -501,7 +501,7 @@ Lane& Model::lane(int i) {
     if (stagger) {
       int least = 0, greatest = 0;
       HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      const int prio = std::min(least, greatest + (int)lanes_.size());
+      const int prio = std::min(least, greatest + prio_base_ + (int)lanes_.size());
       HIP_OK(hipStreamCreateWithPriority(&l->st, hipStreamNonBlocking, prio));
     } else {
       HIP_OK(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));

@@ -225,6 +225,9 @@ class Model {
   void set_synthesis_precision(int p) { gs_fp16_ = p == 1; }
   int synthesis_precision() const { return gs_fp16_ ? 1 : 0; }
   int lanes() const { return nlanes_; }
+  // stream-priority offset of this model's lanes (lane i: greatest + base + i, clamped): request streams
+  // served by separate models get staggered priorities too (applies to lanes created afterwards)
+  void set_priority_base(int b) { prio_base_ = b; }
   // test switch: NaN-fill every arena block on allocation (Arena::poison_on); also $MLIC_POISON=1
   void set_poison(bool on) { poison_ = on; }
   // fp16 range-guard fallbacks taken since the last reset (they change the arithmetic of a call, so the
@@ -274,6 +277,7 @@ class Model {
   std::vector<EncodedImage> enc_all_;
   std::vector<std::unique_ptr<Lane>> lanes_;
   int nlanes_ = 4;
+  int prio_base_ = 0;
   int precision_ = PREC_F16X3_V2;
   bool gs_fp16_ = false;
   HostStats hstats_;

@@ -147,6 +147,8 @@ class MLICPlusPlus(nn.Module):
         self._tables_pushed = None
         if getattr(self, "_lanes", None):
             _lib.call("mlic_set_lanes", h, self._lanes)
+        if getattr(self, "_prio_base", None):
+            _lib.call("mlic_set_priority_base", h, self._prio_base)
         if getattr(self, "_precision", None) is not None:
             _lib.call("mlic_set_precision", h, self._precision)
         if getattr(self, "_synth_precision", None) is not None:
@@ -169,6 +171,12 @@ class MLICPlusPlus(nn.Module):
         self._synth_precision = int(mode)
         if self._handle is not None:
             _lib.call("mlic_set_synthesis_precision", self._handle, self._synth_precision)
+
+    def set_priority_base(self, base: int):
+        """Stream-priority offset of this model's lanes (scheduling only; set before the first call)."""
+        self._prio_base = int(base)
+        if self._handle is not None:
+            _lib.call("mlic_set_priority_base", self._handle, self._prio_base)
 
     def set_lanes(self, n: int):
         """Host threads x HIP streams used by compress()/decompress() (results do not depend on it)."""
