@@ -13,7 +13,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/record}
 KERN=${2:-conv_x4_kernel}
 STAGES=${3:-"tests pmc bench decode rocprof"}
-ISO="--lanes 1 --batch 8 --split 1"
+ISO="--lanes 1 --batch 8 --split 1"  # (with --no-decode-record below: the main region's launches only)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
@@ -29,10 +29,10 @@ if has tests; then
 fi
 if has pmc; then
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 -u bench.py $ISO --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > "$OUT/pmc_fetch.log" 2>&1 ||
+    python3 -u bench.py $ISO --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --no-decode-record > "$OUT/pmc_fetch.log" 2>&1 ||
     { echo "pmc fetch failed $?"; tail -20 "$OUT/pmc_fetch.log"; exit 1; }
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 -u bench.py $ISO --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > "$OUT/pmc_write.log" 2>&1 ||
+    python3 -u bench.py $ISO --steps 1 --warmup 0 --no-cpu-baseline --no-roofline --no-decode-record > "$OUT/pmc_write.log" 2>&1 ||
     { echo "pmc write failed $?"; tail -20 "$OUT/pmc_write.log"; exit 1; }
   python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$KERN" "$OUT/traffic.json" config=main \
     "launches_of=isolated pass: bench.py --lanes 1 --batch 8 --split 1 --steps 1 --warmup 0 (the launches roofline.frac divides by)" || exit 1
@@ -52,11 +52,11 @@ if has decode; then
 fi
 if has rocprof; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_iso" -o run -- \
-    python3 -u bench.py $ISO --steps 2 --warmup 1 --no-cpu-baseline --no-roofline > "$OUT/bench_iso_under_rocprof.json" \
+    python3 -u bench.py $ISO --steps 2 --warmup 1 --no-cpu-baseline --no-roofline --no-decode-record > "$OUT/bench_iso_under_rocprof.json" \
     2> "$OUT/rocprof_iso.err" || { echo "rocprof iso failed $?"; tail -20 "$OUT/rocprof_iso.err"; exit 1; }
   rm -f "$OUT"/prof_iso/run_kernel_trace.csv
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_timed" -o run -- \
-    python3 -u bench.py --no-cpu-baseline --no-roofline > "$OUT/bench_timed_under_rocprof.json" \
+    python3 -u bench.py --no-cpu-baseline --no-roofline --no-decode-record > "$OUT/bench_timed_under_rocprof.json" \
     2> "$OUT/rocprof_timed.err" || { echo "rocprof timed failed $?"; tail -20 "$OUT/rocprof_timed.err"; exit 1; }
   rm -f "$OUT"/prof_timed/run_kernel_trace.csv
 fi
