@@ -116,7 +116,7 @@ def parse(argv=None):
     ap.add_argument("--profile-lanes", type=int, default=0,
                     help="lanes of the profiled step (0 = same as --lanes, so its launches match the timed "
                          "steps' and rocprofv3's per-kernel averages; 1 = isolated per-kernel times)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"),
                     help="PMC-derived HBM bytes per launch of the dominant family (tools/pmc_traffic.py)")
     ap.add_argument("--group-concurrency", type=int, default=0,
                     help="(weights, shape) batches of a step run concurrently, each on its own model "

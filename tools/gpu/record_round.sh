@@ -39,13 +39,13 @@ if has pmc; then
   rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write"
 fi
 if has bench; then
-  TJ="$OUT/traffic.json"; [ -f "$TJ" ] || TJ=profiles/traffic_r05.json
+  TJ="$OUT/traffic.json"; [ -f "$TJ" ] || TJ=profiles/traffic_r06.json
   timeout -k 10 600 python3 -u bench.py --traffic-json "$TJ" --layers-out "$OUT/layers.tsv" \
     > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed $?"; tail -30 "$OUT/bench.err"; exit 1; }
   head -c 400 "$OUT/bench.json"; echo
 fi
 if has decode; then
-  TJ="$OUT/traffic.json"; [ -f "$TJ" ] || TJ=profiles/traffic_r05.json
+  TJ="$OUT/traffic.json"; [ -f "$TJ" ] || TJ=profiles/traffic_r06.json
   timeout -k 10 600 python3 -u bench.py --phase decode --traffic-json "$TJ" > "$OUT/bench_decode.json" \
     2> "$OUT/bench_decode.err" || { echo "bench decode failed $?"; tail -30 "$OUT/bench_decode.err"; exit 1; }
   head -c 300 "$OUT/bench_decode.json"; echo
