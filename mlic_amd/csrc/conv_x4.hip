@@ -21,8 +21,11 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 namespace mlic {
 
@@ -806,7 +809,26 @@ __global__ void x4_pack_weights_kernel(const _Float16* __restrict__ wh, const _F
 // ---------------------------------------------------------------------------------------------
 // 256-row Cout tiles unless 128-row tiles pad at least 1/8 of Cout less (e.g. 320, 640 -> 128)
 int x4_bm(int Cout) {
+  // A/B: $MLIC_X4_BM_FOR="Cout:BM,Cout:BM" forces the tile height of the listed Cout values
+  static const std::vector<std::pair<int, int>> force = [] {
+    std::vector<std::pair<int, int>> v;
+    const char* e = std::getenv("MLIC_X4_BM_FOR");
+    for (const char* q = e; q && *q;) {
+      int c = 0, m = 0, n = 0;
+      if (std::sscanf(q, "%d:%d%n", &c, &m, &n) != 2) break;
+      if (m == 64 || m == 96 || m == 128 || m == 192 || m == 224 || m == 256) v.emplace_back(c, m);
+      q += n;
+      if (*q == ',') ++q;
+    }
+    return v;
+  }();
+  for (const auto& f : force)
+    if (f.first == Cout) return f.second;
   if (Cout <= 64) return 64;
+  // MLICPP_L's h_s 320 -> 1280 subpel conv runs at 1/64 of the image (17 x 30 at 1080p: 24 pixel tiles
+  // per 8 images): 256-row tiles leave half the CUs idle (120 workgroups), 128-row tiles fill them --
+  // 252 -> 157 us (8 x 17 x 30, profiles/r06/ab/x4_tile_height_ab.log); 480 -> 1920 (1/32) is equal either way
+  if (Cout == 1280) return 128;
   static const bool t96 = [] {  // A/B: MLIC_X4_BM96=0 keeps 128-row tiles for Cout 65..96
     const char* e = std::getenv("MLIC_X4_BM96");
     return !(e && e[0] == '0');
