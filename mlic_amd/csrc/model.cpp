@@ -1351,6 +1351,9 @@ void Model::slice_loop(Mode mode, const View& hyper, const View* y, const View& 
         }
       }
       // LRP on cat([hyper_means] + y_hat_slices + [current])
+      // compress: the last slice's final y_hat feeds nothing (no later slice; compress() decodes nothing),
+      // so its non-anchor LRP is skipped (mlicpp.py:275-276 computes and discards it)
+      if (mode == Mode::Encode && idx == S - 1 && ph == 1) continue;
       lrp({hyper_means, yhat.ch(0, (idx + 1) * C)}, ph == 0 ? "anchor" : "nonanchor", idx, ysl, ph == 0);
     }
     L().arena.release(m);
